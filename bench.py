@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Headline benchmark: decoded codewords/s + BER vs Eb/N0, 802.11n (648,1/2), min-sum, 50 iterations.
+
+One step = one decode of a batch of B = 65,536 codewords (per GPU) of one Eb/N0 point, LLRs already
+resident in HBM; steps cycle through the 11 points Eb/N0 = 0:0.5:5 dB (BASELINE.json configs[1]).
+Before timing, one untimed pass over all 11 points produces the BER/BLER curve (error counts on device,
+summed over ranks with an RCCL all-reduce — the only collective; the codeword batches shard with no
+data-path exchange, so scaling is weak).
+
+    python bench.py [--gpus N --steps K --warmup W]                  # N=1
+    torchrun --nproc-per-node N ... bench.py --gpus N ...            # one rank per GPU
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ldpc-sims_amd"))
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes_per_cw(n, E, iters, s_m=4, s_l=4):
+    """the reference's two-array flooding dataflow per codeword:
+    iters*(4*E*s_m + n*s_L) + n*s_L + n."""
+    return iters * (4 * E * s_m + n * s_l) + n * s_l + n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=22)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--code", default="wifi648_12")
+    ap.add_argument("--algo", default="minsum")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=65536, help="codewords per GPU per step")
+    ap.add_argument("--clamp", type=float, default=20.0)
+    ap.add_argument("--alpha", type=float, default=1.0)
+    ap.add_argument("--ebn0", default="0:0.5:5")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--force-generic", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import ldpc_amd
+    from ldpc_amd import _abi
+    from ldpc_amd.codes import Encoder
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+
+    H, qc = ldpc_amd.get_code(args.code)
+    m, n = H.shape
+    k = n - m
+    rate = k / n
+    dec = ldpc_amd.get_decoder(H, local)
+    B = args.batch
+    lo, step_db, hi = (float(x) for x in args.ebn0.split(":"))
+    ebn0 = np.round(np.arange(lo, hi + 1e-9, step_db), 6)
+    lib = _abi.load()
+    stream = torch.cuda.current_stream()
+    st = stream.cuda_stream
+
+    # ---- synthetic data, resident in HBM before timing -------------------------------------------
+    enc = Encoder(H)
+    gen = torch.Generator(device="cuda").manual_seed(args.seed + 7919 * rank)
+    info = torch.randint(0, 2, (B, k), generator=gen, device="cuda", dtype=torch.int32)
+    Gp = torch.from_numpy(enc.generator_parity().astype(np.float32)).cuda()
+    par = torch.remainder(info.float() @ Gp, 2.0).to(torch.uint8)
+    cw = torch.cat([info.to(torch.uint8), par], dim=1).contiguous()
+    llrs = []
+    for i, e in enumerate(ebn0):
+        sigma = float(np.sqrt(1.0 / (2.0 * rate * 10.0 ** (e / 10.0))))
+        x = torch.empty((B, n), dtype=torch.float32, device="cuda")
+        _abi.check(lib.ldpc_awgn_llr(cw.data_ptr(), x.data_ptr(), B, n, sigma, args.seed * 1000 + i, rank * B, st))
+        llrs.append(x)
+    p = dec.params(args.iters, args.algo, args.clamp, args.alpha, 0.0, False, "f32", "p1",
+                   force_generic=args.force_generic, device_ptrs=True)
+    wsb = dec.workspace_bytes(B, p)
+    ws = torch.empty((wsb,), dtype=torch.uint8, device="cuda")
+    bits = torch.empty((B, n), dtype=torch.uint8, device="cuda")
+
+    def step(x):
+        _abi.check(lib.ldpc_decode_ex(dec._h, x.data_ptr(), B, p, bits.data_ptr(), None, None, ws.data_ptr(), wsb, st))
+
+    # ---- BER sweep (untimed; also warms up) --------------------------------------------------------
+    counts = torch.zeros((len(ebn0), 3), dtype=torch.int64, device="cuda")
+    for i in range(len(ebn0)):
+        step(llrs[i])
+        _abi.check(lib.ldpc_count_errors(bits.data_ptr(), cw.data_ptr(), B, n, k, counts[i].data_ptr(), st))
+    if world > 1:
+        dist.all_reduce(counts)  # the one collective: per-point error counters, 24 B x 11 per rank
+    c = counts.cpu().numpy().astype(np.float64)
+    coded_ber = (c[:, 0] / (c[:, 2] * k)).tolist()
+    coded_bler = (c[:, 1] / c[:, 2]).tolist()
+    for w in range(args.warmup):
+        step(llrs[w % len(ebn0)])
+    torch.cuda.synchronize()
+
+    # ---- timed region -------------------------------------------------------------------------------
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for s in range(args.steps):
+        step(llrs[s % len(ebn0)])
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    gpu_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    total_cw = world * args.steps * B
+    value = total_cw / elapsed
+
+    # ---- roofline: algorithmic bytes per decode launch / event-timed launch duration ----
+    E = int(H.sum())
+    bpc = algorithmic_bytes_per_cw(n, E, args.iters)
+    achieved = bpc * B / (gpu_ms * 1e-3) / 1e9
+    peak = 8000.0
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("code") == args.code and tj.get("batch") == B and tj.get("iters") == args.iters \
+                    and tj.get("algo") == args.algo and tj.get("path") == ("generic" if args.force_generic or not dec.qc_z else "qc"):
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(H, args, rate)
+
+    if rank == 0:
+        out = {
+            "metric": "decoded codewords/sec + BER@Eb/N0 sweep, (648,1/2) 50-iter min-sum",
+            "value": value,
+            "unit": "codewords/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: random info bits, systematic 802.11n encoder, BPSK/AWGN LLRs generated on device",
+            "config": {
+                "workload": f"{args.code} {args.algo} {args.iters} iters, B={B} codewords/GPU/step, "
+                            f"Eb/N0 {args.ebn0} dB cycled per step",
+                "code": args.code, "n": n, "k": k, "edges": E, "algo": args.algo, "iters": args.iters,
+                "clamp": args.clamp, "alpha": args.alpha, "batch_per_gpu": B, "global_batch": B * world,
+                "parallelism": f"dp{world} (codeword shards, RCCL all-reduce of error counts only)",
+                "kernel_path": "generic-csr" if (args.force_generic or not dec.qc_z) else f"qc-z{dec.qc_z}",
+            },
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                         "frac": achieved / peak, "traffic": traffic,
+                         "bytes_per_codeword_model": bpc, "launch_ms": gpu_ms},
+            "cpu_baseline": cpu,
+            "ber": {"ebn0_db": ebn0.tolist(), "coded_ber_info": coded_ber, "coded_bler": coded_bler,
+                    "codewords_per_point": int(c[0, 2])},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(H, args, rate):
+    """The CPU oracle (oracle/ldpc_oracle.c, OpenMP over codewords) on a bounded sample of the same
+    workload: same code, algorithm and iteration count, Eb/N0 = 2.5 dB.  CPU comparator only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from ldpc_amd.codes import Encoder
+    rng = np.random.default_rng(5)
+    enc = Encoder(H)
+
+    def sample(Bs):
+        c = enc.encode(rng.integers(0, 2, size=(Bs, enc.k)))
+        sigma = np.sqrt(1.0 / (2 * rate * 10 ** (2.5 / 10)))
+        return (-2.0 * ((1.0 - 2.0 * c) + sigma * rng.standard_normal(c.shape)) / sigma**2).astype(np.float32)
+
+    def run(x):
+        t = time.perf_counter()
+        if args.algo in ("minsum", "ms", "min_sum"):
+            oracle.ms_f32(H, x, args.iters, args.clamp, args.alpha, 0.0)
+        else:
+            oracle.sp_f32(H, x, args.iters, args.clamp)
+        return time.perf_counter() - t
+
+    threads = oracle.num_threads()
+    cal = max(64, 8 * threads)
+    tc = run(sample(cal))
+    Bs = int(min(1 << 17, max(cal, cal * args.cpu_seconds / max(tc, 1e-6))))
+    t = run(sample(Bs))
+    return {"value": Bs / t, "unit": "codewords/s", "cores": threads, "kind": "port",
+            "sample": f"{Bs} codewords of {args.code} {args.algo} {args.iters} iters at Eb/N0 2.5 dB "
+                      f"({t:.1f} s, oracle/ldpc_oracle.c, OpenMP {threads} threads)"}
+
+
+if __name__ == "__main__":
+    main()

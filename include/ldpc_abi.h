@@ -1,0 +1,117 @@
+/*
+ * ldpc_abi.h — C ABI of the MI355X-native LDPC belief-propagation decoder (libldpc_hip.so).
+ *
+ * Plain C: pointers, sizes and ints only; no torch / HIP types in any signature (hip streams are passed
+ * as void*).  Every entry point returns 0 (LDPC_OK) or a negative LDPC_E* code and leaves a message in
+ * ldpc_last_error() (thread-local).  The reference (realjwin/ldpc-sims) has no C surface at all: its
+ * decode boundary is Python.  Each function below names the reference interface it replaces.
+ */
+#ifndef LDPC_ABI_H
+#define LDPC_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ldpc_graph ldpc_graph;
+
+enum {
+    LDPC_OK = 0,
+    LDPC_EINVAL = -1,      /* bad argument (shape, range, null pointer)                */
+    LDPC_EHIP = -2,        /* HIP runtime error (message names the call)                */
+    LDPC_ENOMEM = -3,      /* device allocation failed / workspace too small            */
+    LDPC_EUNSUPPORTED = -4 /* combination of algo/flags not implemented for this graph  */
+};
+
+enum {
+    LDPC_ALGO_TANH_SP = 0, /* the reference's algorithm: bp/bp.py, bp_vc.py, bp_cv.py     */
+    LDPC_ALGO_MIN_SUM = 1, /* normalized/offset min-sum (new; see oracle/ldpc_oracle.c) */
+    LDPC_ALGO_QMIN_SUM = 2 /* integer (quantized-LLR) offset min-sum (new)              */
+};
+
+enum {
+    LDPC_F_EARLY_STOP = 1,    /* stop a codeword once its syndrome is zero                   */
+    LDPC_F_DEVICE_PTRS = 2,   /* llr/bits/soft/iters_used are device pointers (else host)     */
+    LDPC_F_F64 = 4,           /* tanh-SP in float64: llr/soft are double* (reference .double()) */
+    LDPC_F_SOFT_Z = 8,        /* soft_out = z = 0.5*(L + sum c2v) (half posterior LLR, P0/P1)  */
+    LDPC_F_FORCE_GENERIC = 16 /* never use a structure-specialised (QC) kernel                 */
+};
+
+typedef struct {
+    int32_t iters;   /* iterations (maximum when LDPC_F_EARLY_STOP)                         */
+    int32_t algo;    /* LDPC_ALGO_*                                                          */
+    int32_t flags;   /* LDPC_F_*                                                             */
+    float clamp;     /* c2v clamp, the reference's clamp_value (bp/bp.py:47)                 */
+    float alpha;     /* min-sum normalisation (1 = plain min-sum)                            */
+    float beta;      /* min-sum offset (float algo) / integer offset (QMIN_SUM)              */
+    int32_t qmax;    /* QMIN_SUM: message/LLR saturation (15 = 5-bit signed)                 */
+    int32_t app_max; /* QMIN_SUM: posterior saturation                                       */
+    float qstep;     /* QMIN_SUM: LLR quantizer step; q = sat(rint(llr / qstep), qmax)       */
+} ldpc_params;
+
+/* Build a Tanner graph from H in CSR form (rows = checks, ascending columns).  Replaces
+ * generate_masks(H) (pytorch/bp/masking.py:12-147) and BeliefPropagation.__init__ (bp/bp.py:20-39):
+ * the graph is built once and reused, instead of dense E x E masks rebuilt per decode_bits call
+ * (ofdm/ofdm_functions.py:143/145).  If H is the lifting of a base matrix for which a specialised
+ * kernel is compiled in (802.11n codes), the handle carries it. */
+int ldpc_graph_create(int32_t m, int32_t n, int32_t nnz, const int32_t* row_ptr, const int32_t* col_idx,
+                      int32_t device, ldpc_graph** out);
+
+/* Same, from a QC base matrix: shifts[mb*nb] row-major, -1 = null block, lifting size z. */
+int ldpc_graph_create_qc(int32_t mb, int32_t nb, int32_t z, const int32_t* shifts, int32_t device,
+                         ldpc_graph** out);
+
+int ldpc_graph_destroy(ldpc_graph* g);
+
+/* m, n, nnz (=E, the reference's layer_size(), bp/bp.py:61-62), and the QC lifting size of the
+ * specialised kernel in use (0 = generic CSR kernels). */
+int ldpc_graph_info(const ldpc_graph* g, int32_t* m, int32_t* n, int32_t* nnz, int32_t* qc_z);
+
+/* Device bytes ldpc_decode_ex needs as caller-provided workspace for a batch of B codewords. */
+int ldpc_workspace_size(const ldpc_graph* g, int64_t B, const ldpc_params* p, size_t* bytes);
+
+/* Decode B codewords.  Replaces BeliefPropagation.forward(x=0, llr, clamp) -> p1 (bp/bp.py:43-51) and
+ * the batch loop of decode_bits (ofdm/ofdm_functions.py:152-161).
+ *   llr[B][n]     log P(bit=1)/P(bit=0), the reference's convention (ofdm_functions.py:72);
+ *                 float* (double* with LDPC_F_F64).
+ *   bits_out[B][n] 0/1 hard decisions, np.round(p1) semantics (ties -> 0).  May be NULL.
+ *   soft_out[B][n] p1 = 1 - sigmoid(z) (or z with LDPC_F_SOFT_Z); float* (double* with F64).  May be NULL.
+ *   iters_used[B] iterations run per codeword (== iters unless early stop).  May be NULL.
+ *   workspace     device buffer of >= ldpc_workspace_size bytes, or NULL to use a per-graph internal
+ *                 one (then the call is synchronous and serialised per graph).
+ *   stream        hipStream_t as void* (NULL = default stream).  With LDPC_F_DEVICE_PTRS and a caller
+ *                 workspace the call is asynchronous on the stream and graph-capturable; with host
+ *                 pointers it copies in/out and returns after the stream synchronises. */
+int ldpc_decode_ex(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_params* p, uint8_t* bits_out,
+                   void* soft_out, int32_t* iters_used, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Convenience form (float llr, internal workspace). */
+int ldpc_decode(const ldpc_graph* g, const float* llr, int64_t B, int32_t iters, float clamp, int32_t algo,
+                int32_t flags, uint8_t* bits_out, float* soft_out, void* stream);
+
+/* Error counting on device, the metrics of evaluate_quantized.py:139-141 for one SNR point:
+ *   counts[0] += bit errors over the first info_bits positions of each codeword (coded BER numerator)
+ *   counts[1] += codewords with any error over all n positions              (coded BLER numerator)
+ *   counts[2] += B
+ * bits, ref: device uint8 [B][n]; counts: device int64[3] (accumulated, not cleared). */
+int ldpc_count_errors(const uint8_t* bits, const uint8_t* ref, int64_t B, int32_t n, int32_t info_bits,
+                      int64_t* counts, void* stream);
+
+/* BPSK/AWGN channel on device: llr[b][v] = -2 y / sigma^2 with y = (1 - 2 c[b][v]) + sigma * N(0,1),
+ * N from a counter-based generator keyed by (seed, b0 + b, v).  codeword may be NULL (all-zero).
+ * Distributionally equal to the reference's QPSK-OFDM path for rate-1/2 at SNR = Eb/N0
+ * (ofdm_functions.py:17-35,63-78). */
+int ldpc_awgn_llr(const uint8_t* codeword, float* llr, int64_t B, int32_t n, float sigma, uint64_t seed,
+                  int64_t b0, void* stream);
+
+const char* ldpc_last_error(void);
+int ldpc_device_count(void);
+const char* ldpc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDPC_ABI_H */

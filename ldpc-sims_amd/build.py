@@ -1,0 +1,29 @@
+"""Build libldpc_hip.so in-tree for gfx950 (hipcc cross-compiles; no GPU needed)."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRCS = ["abi.hip", "generic.hip", "qc.hip"]
+OUT = os.path.join(HERE, "ldpc_amd", "libldpc_hip.so")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+         "-ffp-contract=off",  # min-sum must round exactly like oracle/ldpc_oracle.c (no FMA contraction)
+         "-Wall", "-Wno-unused-function"]
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    srcs = [os.path.join(HERE, "csrc", s) for s in SRCS]
+    deps = srcs + [os.path.join(HERE, "csrc", "common.h"), os.path.join(ROOT, "include", "ldpc_abi.h")]
+    deps += [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
+    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps):
+        return OUT
+    cmd = ["hipcc", *FLAGS, "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc"), "-o", OUT, *srcs]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,89 @@
+// common.h — shared device/host definitions for the gfx950 LDPC decoder.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ldpc_abi.h"
+
+namespace ldpc {
+
+// Hard-decision thresholds: bit = 1 iff np.round(1 - sigmoid(z)) == 1 (ofdm_functions.py:161, bp.py:51).
+// fp32: measured bit pattern by bit pattern against torch 2.10 CPU sigmoid -> z <= -1.7881392e-07.
+constexpr float kZthrF32 = -1.7881392e-07f;            // 0xb43fffff
+constexpr double kZthrF64 = -3.3306690738754696e-16;   // -1.5 * 2^-52 (strict <)
+// bp_cv.py:258-261: clamp(p, -(1-eps), 1-eps), eps = 1e-7, the bound cast to the tensor dtype.
+constexpr float kPmaxF32 = (float)(1.0 - 1e-7);
+constexpr double kPmaxF64 = 1.0 - 1e-7;
+
+template <typename T> struct Num;
+template <> struct Num<float> {
+    __device__ static float tanh_(float x) { return tanhf(x); }
+    __device__ static float log_(float x) { return logf(x); }
+    __device__ static float exp_(float x) { return expf(x); }
+    static constexpr float pmax = kPmaxF32;
+    __device__ static bool bit(float z) { return z <= kZthrF32; }
+};
+template <> struct Num<double> {
+    __device__ static double tanh_(double x) { return tanh(x); }
+    __device__ static double log_(double x) { return log(x); }
+    __device__ static double exp_(double x) { return exp(x); }
+    static constexpr double pmax = kPmaxF64;
+    __device__ static bool bit(double z) { return z < kZthrF64; }
+};
+
+__device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
+
+// min-sum check-node output magnitude (oracle/ldpc_oracle.c ms_f32_one): min(clamp, max(alpha*m - beta, 0))
+__device__ __forceinline__ float ms_mag(float m, float alpha, float beta, float clamp) {
+    float x = alpha * m;
+    x = fmaxf(x - beta, 0.0f);
+    return fminf(x, clamp);
+}
+
+// ---- counter-based normal generator (Philox-4x32-10 + Box-Muller) for the on-device channel ----
+struct Philox {
+    __device__ static void round_(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0, uint32_t k1) {
+        const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+        uint32_t hi0 = __umulhi(M0, c0), lo0 = M0 * c0;
+        uint32_t hi1 = __umulhi(M1, c2), lo1 = M1 * c2;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    }
+    __device__ static void gen(uint64_t ctr, uint64_t key, uint32_t out[4]) {
+        uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0x5bd1e995u, c3 = 0x1b873593u;
+        uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            round_(c0, c1, c2, c3, k0, k1);
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+    }
+};
+
+}  // namespace ldpc
+
+// internal entry points shared between translation units
+namespace ldpc {
+int set_error(int code, const char* fmt, ...);
+int fill_i32(int32_t* p, int64_t count, int32_t value, hipStream_t st);
+
+struct GenericArgs {
+    const int32_t *row_ptr, *var_ptr, *var_edges;
+    int m, n, E, max_dc, max_dv;
+};
+size_t generic_workspace(int n, int E, int64_t B, size_t elem);
+int generic_decode(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,
+                   void* soft, int32_t* iters_used, char* ws, hipStream_t st);
+
+// Structure-specialised (quasi-cyclic) decoders compiled into the library (qc.hip).
+struct QCSpec;
+const QCSpec* qc_lookup(int mb, int nb, int z, const int32_t* shifts);
+int qc_z(const QCSpec* s);
+bool qc_supports(const QCSpec* s, const ldpc_params& p);
+size_t qc_workspace(const QCSpec* s, int64_t B, const ldpc_params& p);
+int qc_decode(const QCSpec* s, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+              int32_t* iters_used, char* ws, hipStream_t st);
+}  // namespace ldpc

@@ -1,0 +1,78 @@
+"""ctypes binding of libldpc_hip.so (include/ldpc_abi.h).
+
+There is deliberately no fallback: if the HIP library is missing, importing ldpc_amd raises.  The
+decoder exists only as the gfx950 code in ``ldpc-sims_amd/csrc``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libldpc_hip.so"
+LIB_PATH = os.path.join(HERE, LIB_NAME)
+
+LDPC_OK, LDPC_EINVAL, LDPC_EHIP, LDPC_ENOMEM, LDPC_EUNSUPPORTED = 0, -1, -2, -3, -4
+ALGO_TANH_SP, ALGO_MIN_SUM, ALGO_QMIN_SUM = 0, 1, 2
+F_EARLY_STOP, F_DEVICE_PTRS, F_F64, F_SOFT_Z, F_FORCE_GENERIC = 1, 2, 4, 8, 16
+
+# every symbol include/ldpc_abi.h declares (tests/test_abi.py checks the header and the .so agree)
+EXPORTS = (
+    "ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
+    "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
+    "ldpc_last_error", "ldpc_device_count", "ldpc_version",
+)
+
+
+class LdpcError(RuntimeError):
+    """Raised for a non-zero return code; carries ldpc_last_error()."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"ldpc error {code}: {msg}")
+        self.code = code
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("iters", ctypes.c_int32), ("algo", ctypes.c_int32), ("flags", ctypes.c_int32),
+                ("clamp", ctypes.c_float), ("alpha", ctypes.c_float), ("beta", ctypes.c_float),
+                ("qmax", ctypes.c_int32), ("app_max", ctypes.c_int32), ("qstep", ctypes.c_float)]
+
+
+_lib = None
+
+
+def load(path: str | None = None):
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(f"{p} not found: the HIP decoder is not built (run `python __graft_entry__.py`); "
+                          "there is no CPU fallback")
+    L = ctypes.CDLL(p)
+    vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+    gpp = ctypes.POINTER(ctypes.c_void_p)
+    L.ldpc_graph_create.argtypes = [i32, i32, i32, vp, vp, i32, gpp]
+    L.ldpc_graph_create_qc.argtypes = [i32, i32, i32, vp, i32, gpp]
+    L.ldpc_graph_destroy.argtypes = [vp]
+    L.ldpc_graph_info.argtypes = [vp, vp, vp, vp, vp]
+    L.ldpc_workspace_size.argtypes = [vp, i64, ctypes.POINTER(Params), ctypes.POINTER(sz)]
+    L.ldpc_decode_ex.argtypes = [vp, vp, i64, ctypes.POINTER(Params), vp, vp, vp, vp, sz, vp]
+    L.ldpc_decode.argtypes = [vp, vp, i64, i32, ctypes.c_float, i32, i32, vp, vp, vp]
+    L.ldpc_count_errors.argtypes = [vp, vp, i64, i32, i32, vp, vp]
+    L.ldpc_awgn_llr.argtypes = [vp, vp, i64, i32, ctypes.c_float, ctypes.c_uint64, i64, vp]
+    for f in ("ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
+              "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
+              "ldpc_device_count"):
+        getattr(L, f).restype = ctypes.c_int
+    L.ldpc_last_error.restype = ctypes.c_char_p
+    L.ldpc_version.restype = ctypes.c_char_p
+    if path is None:
+        _lib = L
+    return L
+
+
+def check(rc: int):
+    if rc != LDPC_OK:
+        raise LdpcError(rc, load().ldpc_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,240 @@
+"""Python surface of the MI355X decoder, mirroring the reference's decode boundary.
+
+* ``decode_bits(llrs, H, bp_iterations, batch_size, clamp_value)`` — drop-in for
+  ``pytorch/ofdm/ofdm_functions.py:131-163`` (same arguments, float64 0/1 output, rows past
+  ``(N // batch_size) * batch_size`` left 0, tanh sum-product, fp32 arithmetic).
+* ``decoder`` — alias for the same function: the reference's stale scripts call a missing
+  ``decoder(...)`` with these 5 arguments (``evaluate.py:9,117``).
+* ``BeliefPropagation(H, iterations)`` — ``torch.nn.Module`` with ``forward(x, llr, clamp_value) -> p1`` and
+  ``layer_size()``, as ``pytorch/bp/bp.py:19-62`` (used directly by ``ber_test.py:87``).
+* ``decode(H, llr, max_iters, ...)`` — the general entry point (algorithms, precision, early stop,
+  device tensors without host copies).
+
+All arithmetic runs in libldpc_hip.so on the GPU; nothing here computes a message.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import threading
+
+import numpy as np
+
+from . import _abi
+from ._abi import Params, check
+from .codes import Graph
+
+_ALGOS = {"tanh": _abi.ALGO_TANH_SP, "sp": _abi.ALGO_TANH_SP, "tanh_sp": _abi.ALGO_TANH_SP,
+          "minsum": _abi.ALGO_MIN_SUM, "min_sum": _abi.ALGO_MIN_SUM, "ms": _abi.ALGO_MIN_SUM,
+          "qminsum": _abi.ALGO_QMIN_SUM, "qms": _abi.ALGO_QMIN_SUM}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class Decoder:
+    """One Tanner graph resident on one GPU (a ``ldpc_graph`` handle)."""
+
+    def __init__(self, H, device: int = 0):
+        self.lib = _abi.load()
+        H = np.asarray(H)
+        g = Graph.from_H(H)
+        self.m, self.n, self.E = g.m, g.n, g.E
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        rp = np.ascontiguousarray(g.row_ptr, np.int32)
+        ci = np.ascontiguousarray(g.col_idx, np.int32)
+        check(self.lib.ldpc_graph_create(g.m, g.n, g.E, rp.ctypes.data, ci.ctypes.data, self.device, ctypes.byref(h)))
+        self._h = h
+        z = ctypes.c_int32()
+        check(self.lib.ldpc_graph_info(self._h, None, None, None, ctypes.byref(z)))
+        self.qc_z = int(z.value)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.ldpc_graph_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    @staticmethod
+    def params(iters, algo="tanh", clamp=10.0, alpha=1.0, beta=0.0, early_stop=False, precision="f32",
+               soft="p1", qmax=15, app_max=127, qstep=1.0, force_generic=False, device_ptrs=False) -> Params:
+        if algo not in _ALGOS:
+            raise ValueError(f"algo must be one of {sorted(_ALGOS)}")
+        if precision not in ("f32", "f64"):
+            raise ValueError("precision must be 'f32' or 'f64'")
+        flags = 0
+        flags |= _abi.F_EARLY_STOP if early_stop else 0
+        flags |= _abi.F_F64 if precision == "f64" else 0
+        flags |= _abi.F_SOFT_Z if soft == "z" else 0
+        flags |= _abi.F_FORCE_GENERIC if force_generic else 0
+        flags |= _abi.F_DEVICE_PTRS if device_ptrs else 0
+        return Params(int(iters), _ALGOS[algo], flags, float(clamp), float(alpha), float(beta), int(qmax),
+                      int(app_max), float(qstep))
+
+    def workspace_bytes(self, B: int, p: Params) -> int:
+        out = ctypes.c_size_t()
+        check(self.lib.ldpc_workspace_size(self._h, int(B), ctypes.byref(p), ctypes.byref(out)))
+        return int(out.value)
+
+    def decode(self, llr, iters: int, *, algo="tanh", clamp=10.0, alpha=1.0, beta=0.0, early_stop=False,
+               precision="f32", soft=None, qmax=15, app_max=127, qstep=1.0, force_generic=False, stream=None,
+               want_bits=True, want_iters=False):
+        """Decode a (B, n) batch of LLRs (log P1/P0).  numpy in -> numpy out (host staging inside the
+        library); torch GPU tensor in -> torch GPU tensors out, asynchronous on ``stream`` (default: the
+        current torch stream) with a torch-allocated workspace.  Returns dict(bits, soft, iters_used)."""
+        is_torch = type(llr).__module__.startswith("torch")
+        on_gpu = is_torch and llr.is_cuda
+        fdt = np.float64 if precision == "f64" else np.float32
+        p = self.params(iters, algo, clamp, alpha, beta, early_stop, precision, soft or "p1", qmax, app_max,
+                        qstep, force_generic, device_ptrs=on_gpu)
+        if on_gpu:
+            torch = _torch()
+            tdt = torch.float64 if precision == "f64" else torch.float32
+            x = llr.detach().to(tdt).contiguous()
+            if x.dim() != 2 or x.shape[1] != self.n:
+                raise RuntimeError(f"llr must be (B, {self.n}), got {tuple(x.shape)}")
+            B = x.shape[0]
+            dev = x.device
+            bits = torch.empty((B, self.n), dtype=torch.uint8, device=dev) if want_bits else None
+            sft = torch.empty((B, self.n), dtype=tdt, device=dev) if soft else None
+            used = torch.empty((B,), dtype=torch.int32, device=dev) if want_iters else None
+            wsb = self.workspace_bytes(B, p)
+            ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dev)
+            st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+            check(self.lib.ldpc_decode_ex(self._h, x.data_ptr(), B, ctypes.byref(p),
+                                          bits.data_ptr() if bits is not None else None,
+                                          sft.data_ptr() if sft is not None else None,
+                                          used.data_ptr() if used is not None else None, ws.data_ptr(), wsb,
+                                          ctypes.c_void_p(st)))
+            # ws was allocated on the current stream; returning it keeps it alive until the caller drops the
+            # result (torch's allocator then recycles it in stream order).
+            return dict(bits=bits, soft=sft, iters_used=used, workspace=ws)
+        if is_torch:
+            llr = llr.detach().cpu().numpy()
+        x = np.ascontiguousarray(llr, dtype=fdt)
+        if x.ndim != 2 or x.shape[1] != self.n:
+            raise RuntimeError(f"llr must be (B, {self.n}), got {x.shape}")
+        B = x.shape[0]
+        bits = np.empty((B, self.n), np.uint8) if want_bits else None
+        sft = np.empty((B, self.n), fdt) if soft else None
+        used = np.empty((B,), np.int32) if want_iters else None
+        check(self.lib.ldpc_decode_ex(self._h, x.ctypes.data, B, ctypes.byref(p),
+                                      bits.ctypes.data if bits is not None else None,
+                                      sft.ctypes.data if sft is not None else None,
+                                      used.ctypes.data if used is not None else None, None, 0, None))
+        return dict(bits=bits, soft=sft, iters_used=used)
+
+
+_cache: dict = {}
+_cache_lock = threading.Lock()
+
+
+def get_decoder(H, device: int = 0) -> Decoder:
+    """Graphs are built once per (H, device) — the reference rebuilt its dense masks on every
+    decode_bits call (ofdm_functions.py:143/145)."""
+    H = np.asarray(H)
+    key = (H.shape, hashlib.sha1(np.packbits(H.astype(np.uint8) & 1).tobytes()).hexdigest(), int(device))
+    with _cache_lock:
+        d = _cache.get(key)
+        if d is None:
+            d = Decoder(H, device)
+            _cache[key] = d
+        return d
+
+
+def decode(H, llr, max_iters: int, *, algo="tanh", clamp=10.0, alpha=1.0, beta=0.0, early_stop=False,
+           precision="f32", out="bits", device=None, **kw):
+    """``decode(H, llr, max_iters)`` -> hard bits (uint8, (B, n)); ``out="bits+soft"`` -> (bits, p1)."""
+    if device is None:
+        device = llr.device.index if (type(llr).__module__.startswith("torch") and llr.is_cuda) else 0
+    dec = get_decoder(H, device or 0)
+    soft = "p1" if out == "bits+soft" else kw.pop("soft", None)
+    r = dec.decode(llr, max_iters, algo=algo, clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop,
+                   precision=precision, soft=soft, **kw)
+    if out == "bits+soft":
+        return r["bits"], r["soft"]
+    if out == "bits":
+        return r["bits"]
+    return r
+
+
+def decode_bits(llrs, H, bp_iterations, batch_size, clamp_value):
+    """Drop-in for ``decode_bits`` (``pytorch/ofdm/ofdm_functions.py:131-163``).
+
+    Same arguments and conventions: ``llrs`` (N, n) in log P(1)/P(0), converted to float32 as the
+    reference does (``:156``); tanh sum-product for ``bp_iterations`` flooding iterations with messages
+    clamped to ``clamp_value``; returns float64 0.0/1.0 of shape (N, n) where only the first
+    ``(N // batch_size) * batch_size`` rows are decoded and the remainder stays 0 (``:133-135``).
+    """
+    llrs = np.asarray(llrs)
+    output_bits = np.zeros(llrs.shape)
+    num_batches = llrs.shape[0] // batch_size  # ZeroDivisionError for batch_size == 0, as the reference
+    rows = num_batches * batch_size
+    if rows == 0:
+        return output_bits
+    if llrs.ndim != 2 or llrs.shape[1] != np.asarray(H).shape[1]:
+        raise RuntimeError(f"llrs shape {llrs.shape} does not match H {np.asarray(H).shape}")
+    dec = get_decoder(H)
+    chunk = max(batch_size, (1 << 26) // max(dec.E, 1) // batch_size * batch_size)
+    for s in range(0, rows, chunk):
+        e = min(rows, s + chunk)
+        r = dec.decode(llrs[s:e].astype(np.float32), int(bp_iterations), algo="tanh", clamp=float(clamp_value))
+        output_bits[s:e] = r["bits"]
+    return output_bits
+
+
+decoder = decode_bits
+
+
+def _make_bp_module():
+    torch = _torch()
+    nn = torch.nn
+
+    class BeliefPropagation(nn.Module):
+        """``bp/bp.py:19-62`` interface: ``BeliefPropagation(H, iterations)``, ``forward(x, llr, clamp)``
+        returns ``p1 = 1 - sigmoid(z)`` (B, n); ``.double()`` switches to float64 arithmetic like the
+        reference module; ``layer_size()`` = number of edges E.  ``x`` (initial c2v messages, check-order)
+        must be zero, which is what every reference caller passes (``ofdm_functions.py:157``)."""
+
+        def __init__(self, H, iterations):
+            super().__init__()
+            self.H = np.asarray(H)
+            self.iterations = int(iterations)
+            self.layer_size_val = int(np.count_nonzero(self.H))
+            self.register_buffer("_dtype_probe", torch.zeros(1, dtype=torch.float32))
+
+        def layer_size(self):
+            return self.layer_size_val
+
+        def forward(self, x, llr, clamp_value):
+            if x is not None and bool(torch.count_nonzero(x)):
+                raise NotImplementedError("non-zero initial messages x are not supported")
+            precision = "f64" if self._dtype_probe.dtype == torch.float64 else "f32"
+            dev = llr.device.index if llr.is_cuda else (torch.cuda.current_device() if torch.cuda.is_available() else 0)
+            d = get_decoder(self.H, dev or 0)
+            r = d.decode(llr, self.iterations, algo="tanh", clamp=float(clamp_value), precision=precision,
+                         soft="p1", want_bits=False)
+            p1 = r["soft"]
+            if not llr.is_cuda:
+                p1 = torch.from_numpy(p1)
+            return p1
+
+    return BeliefPropagation
+
+
+_BP = None
+
+
+def __getattr__(name):  # lazy so that importing ldpc_amd does not import torch
+    global _BP
+    if name == "BeliefPropagation":
+        if _BP is None:
+            _BP = _make_bp_module()
+        return _BP
+    raise AttributeError(name)

@@ -1,0 +1,283 @@
+"""Parity-check matrices, the Tanner-graph layout shared by every decoder, and encoders.
+
+Reference anchors (realjwin/ldpc-sims, read-only at /root/reference):
+  * ``pytorch/bp/parity.py:7-47``  — the (64,32) PEG code ``H`` (32x64, 96 edges) and ``G = [I; P]``.
+  * ``pytorch/bp/masking.py:84-95`` — edge numbering. ``clookup`` numbers the non-zeros of H row-major
+    (the *check-order* edge id, the layout of the reference's ``x`` tensor); ``vlookup`` numbers them
+    column-major (*var-order* id, the layout of the VC output).  ``Graph`` keeps exactly that numbering:
+    edge id == CSR position, and ``var_edges`` lists, per variable, its check-order edge ids in
+    ascending check order (== the var-order id sequence).
+
+The 802.11n tables below are typed in from IEEE 802.11n-2009 Annex R (no network here, nothing in the
+reference holds them); ``tests/test_codes.py`` checks their structure (dual-diagonal parity part,
+full rank, zero syndrome of encoder output).  Parity for the table contents is therefore *unpinned* by
+the reference (SURVEY.md §7 hard part 4).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from functools import lru_cache
+
+import numpy as np
+
+# ---------------------------------------------------------------------------------------------
+# (64,32) PEG code of the reference (pytorch/bp/parity.py:7-40): column indices of the 3 ones per
+# row.  Data only; tests/test_codes.py compares it against tests/golden/peg64_32.npz, which
+# tests/golden/make_golden.py exported from the reference module itself.
+_PEG64_ROWS = (
+    (0, 16, 32), (0, 17, 33), (1, 16, 34), (1, 18, 35), (2, 17, 36), (2, 19, 37), (3, 18, 38),
+    (3, 20, 39), (4, 19, 40), (4, 21, 41), (5, 20, 42), (5, 22, 43), (6, 21, 44), (6, 23, 45),
+    (7, 22, 46), (7, 24, 47), (8, 23, 48), (8, 25, 49), (9, 24, 50), (9, 26, 51), (10, 25, 52),
+    (10, 27, 53), (11, 26, 54), (11, 28, 55), (12, 27, 56), (12, 29, 57), (13, 28, 58),
+    (13, 30, 59), (14, 29, 60), (14, 31, 61), (15, 30, 62), (15, 31, 63),
+)
+
+
+def peg_64_32() -> np.ndarray:
+    """The reference's only code: (64,32) PEG, H is 32x64 int (``bp/parity.py:7-40``)."""
+    H = np.zeros((32, 64), dtype=np.int64)
+    for r, cols in enumerate(_PEG64_ROWS):
+        H[r, list(cols)] = 1
+    return H
+
+
+def peg_64_32_generator() -> np.ndarray:
+    """``G = [I; P]`` with ``P = H[:, 0:32]`` (``bp/parity.py:42-44``); codeword = G @ info mod 2."""
+    H = peg_64_32()
+    return np.concatenate([np.eye(32, dtype=np.int64), H[:, 0:32]], axis=0)
+
+
+# ---------------------------------------------------------------------------------------------
+# IEEE 802.11n (HT) LDPC base matrices.  Entry = cyclic right-shift of the ZxZ identity, '-' = null.
+_WIFI_TABLES = {
+    (648, "1/2"): (27, """
+ 0  -  -  -  0  0  -  -  0  -  -  0  1  0  -  -  -  -  -  -  -  -  -  -
+22  0  -  - 17  -  0  0 12  -  -  -  -  0  0  -  -  -  -  -  -  -  -  -
+ 6  -  0  - 10  -  -  - 24  -  0  -  -  -  0  0  -  -  -  -  -  -  -  -
+ 2  -  -  0 20  -  -  - 25  0  -  -  -  -  -  0  0  -  -  -  -  -  -  -
+23  -  -  -  3  -  -  -  0  -  9 11  -  -  -  -  0  0  -  -  -  -  -  -
+24  - 23  1 17  -  3  - 10  -  -  -  -  -  -  -  -  0  0  -  -  -  -  -
+25  -  -  -  8  -  -  -  7 18  -  -  0  -  -  -  -  -  0  0  -  -  -  -
+13 24  -  -  0  -  8  -  6  -  -  -  -  -  -  -  -  -  -  0  0  -  -  -
+ 7 20  - 16 22 10  -  - 23  -  -  -  -  -  -  -  -  -  -  -  0  0  -  -
+11  -  -  - 19  -  -  - 13  -  3 17  -  -  -  -  -  -  -  -  -  0  0  -
+25  -  8  - 23 18  - 14  9  -  -  -  -  -  -  -  -  -  -  -  -  -  0  0
+ 3  -  -  - 16  -  -  2 25  5  -  -  1  -  -  -  -  -  -  -  -  -  -  0
+"""),
+    (1296, "2/3"): (54, """
+39 31 22 43  - 40  4  - 11  -  - 50  -  -  -  6  1  0  -  -  -  -  -  -
+25 52 41  2  6  - 14  - 34  -  -  - 24  - 37  -  -  0  0  -  -  -  -  -
+43 31 29  0 21  - 28  -  -  2  -  -  7  - 17  -  -  -  0  0  -  -  -  -
+20 33 48  -  4 13  - 26  -  - 22  -  - 46 42  -  -  -  -  0  0  -  -  -
+45  7 18 51 12 25  -  -  - 50  -  -  5  -  -  -  0  -  -  -  0  0  -  -
+35 40 32 16  5  -  - 18  -  - 43 51  - 32  -  -  -  -  -  -  -  0  0  -
+ 9 24 13 22 28  -  - 37  -  - 25  -  - 52  - 13  -  -  -  -  -  -  0  0
+32 22  4 21 16  -  -  - 27 28  - 38  -  -  -  8  1  -  -  -  -  -  -  0
+"""),
+    (1944, "5/6"): (81, """
+13 48 80 66  4 74  7 30 76 52 37 60  - 49 73 31 74 73 23  -  1  0  -  -
+69 63 74 56 64 77 57 65  6 16 51  - 64  - 68  9 48 62 54 27  -  0  0  -
+51 15  0 80 24 25 42 54 44 71 71  9 67 35  - 58  - 29  - 53  0  -  0  0
+16 29 36 41 44 56 59 37 50 24  - 65  4 65 52  -  4  - 73 52  1  -  -  0
+"""),
+}
+
+
+def _parse_base(text: str) -> np.ndarray:
+    rows = [r.split() for r in text.strip().splitlines()]
+    return np.array([[-1 if t == "-" else int(t) for t in r] for r in rows], dtype=np.int32)
+
+
+@dataclass(frozen=True)
+class QCCode:
+    """A quasi-cyclic code: base matrix of shifts (``-1`` = null block) lifted by ``Z``."""
+
+    base: np.ndarray  # (mb, nb) int32
+    Z: int
+    name: str = ""
+
+    @property
+    def mb(self) -> int:
+        return int(self.base.shape[0])
+
+    @property
+    def nb(self) -> int:
+        return int(self.base.shape[1])
+
+    @property
+    def n(self) -> int:
+        return self.nb * self.Z
+
+    @property
+    def m(self) -> int:
+        return self.mb * self.Z
+
+    @property
+    def k(self) -> int:
+        return self.n - self.m
+
+    def H(self) -> np.ndarray:
+        return qc_expand(self.base, self.Z)
+
+
+def qc_expand(base: np.ndarray, Z: int) -> np.ndarray:
+    """Lift a base matrix: block (r, j) with shift s puts a 1 at (r*Z+i, j*Z+(i+s) mod Z)."""
+    base = np.asarray(base)
+    mb, nb = base.shape
+    H = np.zeros((mb * Z, nb * Z), dtype=np.int64)
+    i = np.arange(Z)
+    for r in range(mb):
+        for j in range(nb):
+            s = int(base[r, j])
+            if s >= 0:
+                H[r * Z + i, j * Z + (i + s) % Z] = 1
+    return H
+
+
+def wifi_code(n: int, rate: str) -> QCCode:
+    """IEEE 802.11n LDPC code by block length and rate string, e.g. ``wifi_code(648, "1/2")``."""
+    try:
+        Z, text = _WIFI_TABLES[(int(n), rate)]
+    except KeyError:
+        raise ValueError(f"802.11n code ({n},{rate}) not embedded; have {sorted(_WIFI_TABLES)}") from None
+    return QCCode(_parse_base(text), Z, name=f"wifi{n}_{rate.replace('/', '')}")
+
+
+def available_codes():
+    return ["peg64_32"] + [f"wifi{n}_{r.replace('/', '')}" for (n, r) in sorted(_WIFI_TABLES)]
+
+
+def get_code(name: str):
+    """Return ``(H, qc)`` for a named code; ``qc`` is the QCCode or ``None``."""
+    if name == "peg64_32":
+        return peg_64_32(), None
+    if name.startswith("wifi"):
+        body = name[4:]
+        n, r = body.split("_")
+        rate = f"{r[0]}/{r[1:]}"
+        qc = wifi_code(int(n), rate)
+        return qc.H(), qc
+    raise ValueError(f"unknown code {name!r}; have {available_codes()}")
+
+
+# ---------------------------------------------------------------------------------------------
+@dataclass
+class Graph:
+    """CSR (check-major) Tanner graph with the reference's edge numbering.
+
+    ``row_ptr[m+1]``, ``col_idx[E]``: edges of check c are ``row_ptr[c]..row_ptr[c+1]`` with ascending
+    variable index (``masking.py:44-47,84-88``).  ``var_ptr[n+1]``, ``var_edges[E]``: the check-order
+    edge ids of variable v in ascending check order (``masking.py:52-55,91-95``), so position
+    ``var_ptr[v]+t`` is the reference's var-order edge id.
+    """
+
+    m: int
+    n: int
+    row_ptr: np.ndarray
+    col_idx: np.ndarray
+    var_ptr: np.ndarray
+    var_edges: np.ndarray
+    edge_check: np.ndarray = field(repr=False, default=None)
+
+    @property
+    def E(self) -> int:
+        return int(self.col_idx.shape[0])
+
+    @classmethod
+    def from_H(cls, H) -> "Graph":
+        H = np.asarray(H)
+        if H.ndim != 2:
+            raise ValueError("H must be a 2-D 0/1 matrix")
+        if not np.isin(H, (0, 1)).all():
+            raise ValueError("H must contain only 0/1")
+        m, n = H.shape
+        rows, cols = np.nonzero(H)  # row-major order == clookup order
+        row_ptr = np.zeros(m + 1, dtype=np.int32)
+        np.add.at(row_ptr, rows + 1, 1)
+        row_ptr = np.cumsum(row_ptr).astype(np.int32)
+        col_idx = cols.astype(np.int32)
+        # var-order: stable sort of edge ids by column keeps ascending check order within a column
+        order = np.argsort(cols, kind="stable").astype(np.int32)
+        var_ptr = np.zeros(n + 1, dtype=np.int32)
+        np.add.at(var_ptr, cols + 1, 1)
+        var_ptr = np.cumsum(var_ptr).astype(np.int32)
+        return cls(m, n, row_ptr, col_idx, var_ptr, order, rows.astype(np.int32))
+
+    def check_degrees(self) -> np.ndarray:
+        return np.diff(self.row_ptr)
+
+    def var_degrees(self) -> np.ndarray:
+        return np.diff(self.var_ptr)
+
+
+# ---------------------------------------------------------------------------------------------
+def _gf2_solve_right(B: np.ndarray, A: np.ndarray) -> np.ndarray:
+    """Return X with B @ X = A (mod 2) for square invertible B (uint8 dense, row ops)."""
+    m = B.shape[0]
+    M = np.concatenate([B, A], axis=1).astype(np.uint8) & 1
+    for c in range(m):
+        piv = np.nonzero(M[c:, c])[0]
+        if piv.size == 0:
+            raise np.linalg.LinAlgError("parity part of H is singular over GF(2)")
+        p = c + int(piv[0])
+        if p != c:
+            M[[c, p]] = M[[p, c]]
+        hit = np.nonzero(M[:, c])[0]
+        hit = hit[hit != c]
+        if hit.size:
+            M[hit] ^= M[c]
+    return M[:, m:]
+
+
+@lru_cache(maxsize=16)
+def _parity_map_cached(key: bytes, shape: tuple) -> np.ndarray:
+    H = np.frombuffer(key, dtype=np.uint8).reshape(shape)
+    m, n = H.shape
+    k = n - m
+    return _gf2_solve_right(H[:, k:], H[:, :k])  # (m, k): parity = Pm @ info
+
+
+def gf2_rank(H) -> int:
+    M = (np.asarray(H) & 1).astype(np.uint8).copy()
+    r = 0
+    rows, cols = M.shape
+    for c in range(cols):
+        piv = np.nonzero(M[r:, c])[0]
+        if piv.size == 0:
+            continue
+        p = r + int(piv[0])
+        if p != r:
+            M[[r, p]] = M[[p, r]]
+        hit = np.nonzero(M[:, c])[0]
+        hit = hit[hit != r]
+        if hit.size:
+            M[hit] ^= M[r]
+        r += 1
+        if r == rows:
+            break
+    return r
+
+
+class Encoder:
+    """Systematic encoder for H = [A | B] with the last m columns invertible (802.11n, PEG).
+
+    codeword = [info ; B^-1 A info] (mod 2), i.e. information bits first — the layout of the
+    reference's ``G = [I; P]`` (``bp/parity.py:44``) and of the 802.11n codes.
+    """
+
+    def __init__(self, H):
+        H = (np.asarray(H) & 1).astype(np.uint8)
+        self.m, self.n = H.shape
+        self.k = self.n - self.m
+        self.P = _parity_map_cached(H.tobytes(), H.shape)  # (m, k) uint8
+
+    def encode(self, info: np.ndarray) -> np.ndarray:
+        info = np.asarray(info).astype(np.int64) & 1
+        if info.ndim == 1:
+            info = info[None, :]
+        par = (info @ self.P.T.astype(np.int64)) & 1
+        return np.concatenate([info, par], axis=1).astype(np.uint8)
+
+    def generator_parity(self) -> np.ndarray:
+        """(k, m) matrix Gp with parity = info @ Gp mod 2 (for device-side encoding)."""
+        return self.P.T.copy()

@@ -1,0 +1,350 @@
+/*
+ * ldpc_oracle.c — CPU ORACLE for the LDPC belief-propagation hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library, and only
+ * as the checker / CPU comparator.  The product path (ldpc-sims_amd/, libldpc_hip.so) never calls it.
+ *
+ * It restates, edge by edge, what the reference's dense-mask network computes
+ * (realjwin/ldpc-sims @ /root/reference/pytorch):
+ *
+ *   bp/bp.py:43-51   forward: for it in iters: x = CV(tanh(VC([x, -llr]))).clamp(+-clamp)
+ *                    then p1 = 1 - sigmoid(VC_final([x, -llr]))
+ *   bp/bp_vc.py:16-27 VC: v2c[e=(c,v)] = 0.5 * (L_v + sum_{c' != c} x[(c',v)])   (L = -llr)
+ *                    computed there as a masked mm; every mask weight is exactly 1, so the value is the
+ *                    plain sum, accumulated here in ascending check order (the mm's k order).
+ *   bp/bp_cv.py:22-50 CV: p = prod_{v' != v} tanh(v2c[(c,v')]); p = clamp(p, +-(1-1e-7));
+ *                    x = log((1+p)/(1-p))
+ *   ofdm/ofdm_functions.py:161  bits = np.round(p1): bit 1 iff p1 > 0.5 (ties -> 0).  In fp32 that is
+ *                    exactly z <= -1.7881392e-07 (0xb43fffff) for torch 2.10's CPU sigmoid; measured
+ *                    bit-pattern by bit-pattern in this container (see DESIGN.md "hard decision").
+ *
+ * Edge numbering is the reference's check-order id (bp/masking.py:84-88): CSR position.
+ *
+ * Min-sum (ldpc_ms_*) is NOT in the reference: its specification lives here and in
+ * DESIGN.md, and the GPU kernels must match it bit for bit.  Parity of min-sum against the reference is
+ * unpinned by construction.
+ *
+ *   APP_v = L_v + sum_{e in v, ascending check} c2v[e]           (c2v = 0 before iteration 0)
+ *   v2c_e = APP_v - c2v[e]
+ *   check c: min1 <= min2 the two smallest |v2c| (idx = first edge attaining min1), sgn = xor of sign bits
+ *   c2v[e] = (sgn ^ signbit(v2c_e)) ? -mag : mag,  mag = min(clamp, max(alpha*m - beta, 0)),
+ *            m = (e == idx) ? min2 : min1
+ *   after the last iteration: z_v = 0.5 * APP_v, bit = z_v <= ZTHR (same rule as tanh-SP).
+ *   early stop (flag): after each iteration's APP, stop the codeword when H*bits = 0.
+ *
+ * Quantized min-sum (ldpc_qms_*): integer LLRs in [-qmax, qmax] (the caller quantizes), integer messages
+ * saturated to +-qmax, APP saturated to +-app_max, offset beta (integer), no alpha; bit = APP < 0.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ZTHR_F32 (-1.7881392e-07f)                    /* 0xb43fffff */
+#define ZTHR_F64 (-3.3306690738754696e-16)            /* -1.5 * 2^-52 */
+#define PMAX_F32 ((float)(1.0 - 1e-7))                /* torch casts the python bound to fp32 */
+#define PMAX_F64 (1.0 - 1e-7)
+
+typedef struct {
+    int m, n, E;
+    const int32_t *row_ptr, *col_idx, *var_ptr, *var_edges;
+} graph_t;
+
+/* ------------------------------------------------------------------------------------------ */
+/* tanh sum-product, fp32 (bp/bp.py:43-51, bp_vc.py:16-27, bp_cv.py:22-50)                      */
+static void sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp, float* x, float* v2c,
+                       float* p1_out, float* z_out, uint8_t* bits_out, float* trace, int64_t trace_stride) {
+    const int E = g->E;
+    for (int e = 0; e < E; ++e) x[e] = 0.0f;
+    for (int it = 0; it < iters; ++it) {
+        /* VC + tanh: v2c at check-order ids */
+        for (int v = 0; v < g->n; ++v) {
+            const int a = g->var_ptr[v], b = g->var_ptr[v + 1];
+            const float L = -llr[v];
+            for (int t = a; t < b; ++t) {
+                float S = 0.0f;
+                for (int u = a; u < b; ++u)
+                    if (u != t) S += x[g->var_edges[u]];
+                v2c[g->var_edges[t]] = tanhf(0.5f * (L + S));
+            }
+        }
+        /* CV */
+        for (int c = 0; c < g->m; ++c) {
+            const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
+            for (int e = a; e < b; ++e) {
+                float p = 1.0f;
+                for (int u = a; u < b; ++u)
+                    if (u != e) p *= v2c[u];
+                if (p > PMAX_F32) p = PMAX_F32;
+                if (p < -PMAX_F32) p = -PMAX_F32;
+                float y = logf((1.0f + p) / (1.0f - p));
+                if (y > clamp) y = clamp;
+                if (y < -clamp) y = -clamp;
+                x[e] = y;
+            }
+        }
+        if (trace) memcpy(trace + (int64_t)it * trace_stride, x, sizeof(float) * E);
+    }
+    for (int v = 0; v < g->n; ++v) {
+        float S = 0.0f;
+        for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += x[g->var_edges[u]];
+        const float z = 0.5f * (-llr[v] + S);
+        if (z_out) z_out[v] = z;
+        if (p1_out) p1_out[v] = 1.0f - 1.0f / (1.0f + expf(-z));
+        if (bits_out) bits_out[v] = (uint8_t)(z <= ZTHR_F32);
+    }
+}
+
+/* tanh sum-product, fp64: the reference module after .double() */
+static void sp_f64_one(const graph_t* g, const double* llr, int iters, double clamp, double* x, double* v2c,
+                       double* p1_out, double* z_out, uint8_t* bits_out) {
+    const int E = g->E;
+    for (int e = 0; e < E; ++e) x[e] = 0.0;
+    for (int it = 0; it < iters; ++it) {
+        for (int v = 0; v < g->n; ++v) {
+            const int a = g->var_ptr[v], b = g->var_ptr[v + 1];
+            const double L = -llr[v];
+            for (int t = a; t < b; ++t) {
+                double S = 0.0;
+                for (int u = a; u < b; ++u)
+                    if (u != t) S += x[g->var_edges[u]];
+                v2c[g->var_edges[t]] = tanh(0.5 * (L + S));
+            }
+        }
+        for (int c = 0; c < g->m; ++c) {
+            const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
+            for (int e = a; e < b; ++e) {
+                double p = 1.0;
+                for (int u = a; u < b; ++u)
+                    if (u != e) p *= v2c[u];
+                if (p > PMAX_F64) p = PMAX_F64;
+                if (p < -PMAX_F64) p = -PMAX_F64;
+                double y = log((1.0 + p) / (1.0 - p));
+                if (y > clamp) y = clamp;
+                if (y < -clamp) y = -clamp;
+                x[e] = y;
+            }
+        }
+    }
+    for (int v = 0; v < g->n; ++v) {
+        double S = 0.0;
+        for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += x[g->var_edges[u]];
+        const double z = 0.5 * (-llr[v] + S);
+        if (z_out) z_out[v] = z;
+        if (p1_out) p1_out[v] = 1.0 - 1.0 / (1.0 + exp(-z));
+        if (bits_out) bits_out[v] = (uint8_t)(z < ZTHR_F64);
+    }
+}
+
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+static int syndrome_ok(const graph_t* g, const uint8_t* bits) {
+    for (int c = 0; c < g->m; ++c) {
+        int par = 0;
+        for (int e = g->row_ptr[c]; e < g->row_ptr[c + 1]; ++e) par ^= bits[g->col_idx[e]];
+        if (par) return 0;
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* min-sum, fp32 (specification above; no reference counterpart)                               */
+static int ms_f32_one(const graph_t* g, const float* llr, int iters, float clamp, float alpha, float beta,
+                      int early_stop, float* c2v, float* app, uint8_t* hb, float* p1_out, float* z_out,
+                      uint8_t* bits_out) {
+    const int E = g->E, n = g->n;
+    for (int e = 0; e < E; ++e) c2v[e] = 0.0f;
+    for (int v = 0; v < n; ++v) {
+        float s = -llr[v];
+        for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) s += c2v[g->var_edges[u]];
+        app[v] = s;
+    }
+    int used = 0;
+    for (int it = 0; it < iters; ++it) {
+        for (int c = 0; c < g->m; ++c) {
+            const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
+            float min1 = INFINITY, min2 = INFINITY;
+            int idx = -1;
+            uint32_t sgn = 0;
+            for (int e = a; e < b; ++e) {
+                const float t = app[g->col_idx[e]] - c2v[e];
+                const float m = fabsf(t);
+                sgn ^= f2u(t);
+                if (m < min1) { min2 = min1; min1 = m; idx = e; }
+                else if (m < min2) { min2 = m; }
+            }
+            sgn &= 0x80000000u;
+            for (int e = a; e < b; ++e) {
+                const float t = app[g->col_idx[e]] - c2v[e]; /* recomputed from the OLD c2v[e] */
+                float mag = (e == idx) ? min2 : min1;
+                mag = alpha * mag;
+                mag = fmaxf(mag - beta, 0.0f);
+                mag = fminf(mag, clamp);
+                c2v[e] = u2f(f2u(mag) | ((sgn ^ f2u(t)) & 0x80000000u));
+            }
+        }
+        for (int v = 0; v < n; ++v) {
+            float s = -llr[v];
+            for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) s += c2v[g->var_edges[u]];
+            app[v] = s;
+        }
+        used = it + 1;
+        if (early_stop) {
+            for (int v = 0; v < n; ++v) hb[v] = (uint8_t)(0.5f * app[v] <= ZTHR_F32);
+            if (syndrome_ok(g, hb)) break;
+        }
+    }
+    for (int v = 0; v < n; ++v) {
+        const float z = 0.5f * app[v];
+        if (z_out) z_out[v] = z;
+        if (p1_out) p1_out[v] = 1.0f - 1.0f / (1.0f + expf(-z));
+        if (bits_out) bits_out[v] = (uint8_t)(z <= ZTHR_F32);
+    }
+    return used;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* quantized (integer) offset min-sum: llr already quantized to int8 in [-qmax, qmax]           */
+static inline int sat(int x, int lim) { return x > lim ? lim : (x < -lim ? -lim : x); }
+
+static int qms_one(const graph_t* g, const int8_t* qllr, int iters, int qmax, int app_max, int beta,
+                   int early_stop, int8_t* c2v, int16_t* app, uint8_t* hb, int16_t* app_out, uint8_t* bits_out) {
+    const int E = g->E, n = g->n;
+    for (int e = 0; e < E; ++e) c2v[e] = 0;
+    for (int v = 0; v < n; ++v) app[v] = (int16_t)sat(-(int)qllr[v], app_max);
+    int used = 0;
+    for (int it = 0; it < iters; ++it) {
+        for (int c = 0; c < g->m; ++c) {
+            const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
+            int min1 = 1 << 30, min2 = 1 << 30, idx = -1, sgn = 0;
+            for (int e = a; e < b; ++e) {
+                const int t = sat((int)app[g->col_idx[e]] - (int)c2v[e], qmax);
+                const int m = t < 0 ? -t : t;
+                sgn ^= (t < 0);
+                if (m < min1) { min2 = min1; min1 = m; idx = e; }
+                else if (m < min2) { min2 = m; }
+            }
+            for (int e = a; e < b; ++e) {
+                const int t = sat((int)app[g->col_idx[e]] - (int)c2v[e], qmax);
+                int mag = (e == idx) ? min2 : min1;
+                mag = mag - beta;
+                if (mag < 0) mag = 0;
+                if (mag > qmax) mag = qmax;
+                c2v[e] = (int8_t)((sgn ^ (t < 0)) ? -mag : mag);
+            }
+        }
+        for (int v = 0; v < n; ++v) {
+            int s = -(int)qllr[v];
+            for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) s += c2v[g->var_edges[u]];
+            app[v] = (int16_t)sat(s, app_max);
+        }
+        used = it + 1;
+        if (early_stop) {
+            for (int v = 0; v < n; ++v) hb[v] = (uint8_t)(app[v] < 0);
+            if (syndrome_ok(g, hb)) break;
+        }
+    }
+    for (int v = 0; v < n; ++v) {
+        if (app_out) app_out[v] = app[v];
+        if (bits_out) bits_out[v] = (uint8_t)(app[v] < 0);
+    }
+    return used;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* exported entry points (ctypes).  All arrays row-major [B][n]; outputs may be NULL.             */
+#define GRAPH_ARGS int m, int n, int E, const int32_t *row_ptr, const int32_t *col_idx, \
+                   const int32_t *var_ptr, const int32_t *var_edges
+#define MAKE_GRAPH graph_t g = {m, n, E, row_ptr, col_idx, var_ptr, var_edges}
+
+int oracle_sp_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clamp, float* p1, float* z,
+                  uint8_t* bits, float* trace /* [iters][B][E] or NULL */) {
+    MAKE_GRAPH;
+#pragma omp parallel
+    {
+        float* x = (float*)malloc(sizeof(float) * (size_t)E);
+        float* v2c = (float*)malloc(sizeof(float) * (size_t)E);
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t i = 0; i < B; ++i)
+            sp_f32_one(&g, llr + i * n, iters, clamp, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
+                       bits ? bits + i * n : NULL, trace ? trace + i * E : NULL, B * (int64_t)E);
+        free(x);
+        free(v2c);
+    }
+    return 0;
+}
+
+int oracle_sp_f64(GRAPH_ARGS, const double* llr, int64_t B, int iters, double clamp, double* p1, double* z,
+                  uint8_t* bits) {
+    MAKE_GRAPH;
+#pragma omp parallel
+    {
+        double* x = (double*)malloc(sizeof(double) * (size_t)E);
+        double* v2c = (double*)malloc(sizeof(double) * (size_t)E);
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t i = 0; i < B; ++i)
+            sp_f64_one(&g, llr + i * n, iters, clamp, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
+                       bits ? bits + i * n : NULL);
+        free(x);
+        free(v2c);
+    }
+    return 0;
+}
+
+int oracle_ms_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clamp, float alpha, float beta,
+                  int early_stop, float* p1, float* z, uint8_t* bits, int32_t* iters_used) {
+    MAKE_GRAPH;
+#pragma omp parallel
+    {
+        float* c2v = (float*)malloc(sizeof(float) * (size_t)E);
+        float* app = (float*)malloc(sizeof(float) * (size_t)n);
+        uint8_t* hb = (uint8_t*)malloc((size_t)n);
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t i = 0; i < B; ++i) {
+            int u = ms_f32_one(&g, llr + i * n, iters, clamp, alpha, beta, early_stop, c2v, app, hb,
+                               p1 ? p1 + i * n : NULL, z ? z + i * n : NULL, bits ? bits + i * n : NULL);
+            if (iters_used) iters_used[i] = u;
+        }
+        free(c2v);
+        free(app);
+        free(hb);
+    }
+    return 0;
+}
+
+int oracle_qms(GRAPH_ARGS, const int8_t* qllr, int64_t B, int iters, int qmax, int app_max, int beta,
+               int early_stop, int16_t* app_out, uint8_t* bits, int32_t* iters_used) {
+    MAKE_GRAPH;
+#pragma omp parallel
+    {
+        int8_t* c2v = (int8_t*)malloc((size_t)E);
+        int16_t* app = (int16_t*)malloc(sizeof(int16_t) * (size_t)n);
+        uint8_t* hb = (uint8_t*)malloc((size_t)n);
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t i = 0; i < B; ++i) {
+            int u = qms_one(&g, qllr + i * n, iters, qmax, app_max, beta, early_stop, c2v, app, hb,
+                            app_out ? app_out + i * n : NULL, bits ? bits + i * n : NULL);
+            if (iters_used) iters_used[i] = u;
+        }
+        free(c2v);
+        free(app);
+        free(hb);
+    }
+    return 0;
+}
+
+int oracle_num_threads(void) {
+    int t = 1;
+#pragma omp parallel
+    {
+#pragma omp master
+        {
+#ifdef _OPENMP
+            extern int omp_get_num_threads(void);
+            t = omp_get_num_threads();
+#endif
+        }
+    }
+    return t;
+}

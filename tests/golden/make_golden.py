@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ by running the REFERENCE decoder itself.
+
+Run in the build container only (needs /root/reference; never on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What it records (all .npz, numeric arrays only — loadable with allow_pickle=False):
+  * peg64_32.npz           H and G exported from ``bp/parity.py:7-44``.
+  * bp_peg64_*.npz         For Eb/N0 {0,2,4} dB x (iters, clamp) in {(3,20),(5,10),(10,10),(10,100),(50,10)}:
+                           the input llr (float32, log P1/P0 convention), the reference's fp32 output
+                           ``p1 = BeliefPropagation(H, iters)(0, llr, clamp)`` (``bp/bp.py:43-51``), the same
+                           module run in float64 (``.double()``), and ``np.round(p1)`` hard bits.
+  * bp_peg64_trace.npz     Per-iteration c2v messages ``x`` (check-order, ``bp/bp.py:46-47``) for 16 codewords,
+                           5 iterations, clamp 10 — pins edge ordering and the c2v update itself.
+  * decode_bits_peg64.npz  ``decode_bits(llrs, H, 5, 48, 10)`` (``ofdm/ofdm_functions.py:131-163``) with N=100,
+                           so rows 96..99 (N % batch_size) exercise the "remainder rows stay 0" quirk.
+  * bp_wifi648.npz         802.11n (648,1/2) H (ldpc_amd.codes) through the reference BP: 16 codewords,
+                           iters 5, clamp 10, Eb/N0 1 and 2 dB, fp32 and fp64.
+  * demod_ofdm.npz         ``demodulate_signal`` (``ofdm_functions.py:63-78``) on a fixed received vector:
+                           pins the reference's LLR formula/sign convention for the channel front end.
+"""
+import os
+import sys
+
+os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+sys.dont_write_bytecode = True
+REF = "/root/reference/pytorch"
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.join(ROOT, "ldpc-sims_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+np.complex = complex  # the reference uses np.complex/np.float (removed in numpy 2); in-process shim only
+np.float = float
+
+from bp.bp import BeliefPropagation  # noqa: E402
+from bp import parity  # noqa: E402
+from ofdm import ofdm_functions as OF  # noqa: E402
+
+from ldpc_amd.codes import wifi_code, Encoder  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def bpsk_awgn_llr(code_bits: np.ndarray, ebn0_db: float, rate: float, rng) -> np.ndarray:
+    """BPSK s = 1-2c, y = s + sigma n, sigma^2 = 1/(2 R Eb/N0); LLR log P1/P0 = -2y/sigma^2."""
+    sigma2 = 1.0 / (2.0 * rate * 10.0 ** (ebn0_db / 10.0))
+    y = (1.0 - 2.0 * code_bits) + np.sqrt(sigma2) * rng.standard_normal(code_bits.shape)
+    return (-2.0 * y / sigma2).astype(np.float32)
+
+
+def run_ref(H, iters, clamp, llr32, double=False, trace=False):
+    model = BeliefPropagation(H, iters)
+    model.eval()
+    dtype = torch.float64 if double else torch.float32
+    if double:
+        model = model.double()
+    llr = torch.tensor(llr32, dtype=dtype)
+    x = torch.zeros(llr.shape[0], model.layer_size(), dtype=dtype)
+    snaps = []
+    with torch.no_grad():
+        if trace:  # re-run the forward loop exactly as bp.py:46-51 does, keeping x after each layer
+            for layer in model.layers:
+                x = layer([x, -llr]).clamp(-clamp, clamp)
+                snaps.append(x.numpy().copy())
+            p1 = -1 * model.final_layer([x, -llr]) + 1
+        else:
+            p1 = model(x, llr, clamp)
+    return p1.numpy(), (np.stack(snaps) if trace else None)
+
+
+def main():
+    H = parity.H.astype(np.int64)
+    G = parity.G.astype(np.int64)
+    np.savez_compressed(os.path.join(HERE, "peg64_32.npz"), H=H, G=G)
+
+    B = 128
+    configs = [(3, 20), (5, 10), (10, 10), (10, 100), (50, 10)]
+    for si, snr in enumerate([0.0, 2.0, 4.0]):
+        rng = np.random.default_rng(1000 + si)
+        info = rng.integers(0, 2, size=(B, 32))
+        cw = (info @ G.T) % 2  # G = [I; P]: codeword = G @ info (ofdm_functions.encode_bits:11-15)
+        llr = bpsk_awgn_llr(cw, snr, 0.5, rng)
+        for iters, clamp in configs:
+            p1_32, _ = run_ref(H, iters, clamp, llr)
+            p1_64, _ = run_ref(H, iters, clamp, llr, double=True)
+            name = f"bp_peg64_snr{int(snr)}_it{iters}_cl{clamp}.npz"
+            np.savez_compressed(
+                os.path.join(HERE, name), H=H, llr=llr, codeword=cw.astype(np.uint8), iters=iters,
+                clamp=clamp, p1_f32=p1_32.astype(np.float32), p1_f64=p1_64,
+                bits_f32=np.round(p1_32).astype(np.uint8), bits_f64=np.round(p1_64).astype(np.uint8))
+            print(name, "bit errors vs codeword:", int((np.round(p1_32) != cw).sum()))
+
+    # per-iteration c2v trace (check-order x), 16 codewords
+    rng = np.random.default_rng(77)
+    info = rng.integers(0, 2, size=(16, 32))
+    cw = (info @ G.T) % 2
+    llr = bpsk_awgn_llr(cw, 1.0, 0.5, rng)
+    p1_32, tr32 = run_ref(H, 5, 10, llr, trace=True)
+    p1_64, tr64 = run_ref(H, 5, 10, llr, double=True, trace=True)
+    np.savez_compressed(os.path.join(HERE, "bp_peg64_trace.npz"), H=H, llr=llr, iters=5, clamp=10,
+                        x_f32=tr32.astype(np.float32), x_f64=tr64, p1_f32=p1_32, p1_f64=p1_64)
+
+    # the drop-in boundary itself, with a ragged tail (N % batch_size != 0)
+    rng = np.random.default_rng(99)
+    info = rng.integers(0, 2, size=(100, 32))
+    cw = (info @ G.T) % 2
+    llr64 = bpsk_awgn_llr(cw, 2.0, 0.5, rng).astype(np.float64)
+    out = OF.decode_bits(llr64, H, 5, 48, 10)
+    np.savez_compressed(os.path.join(HERE, "decode_bits_peg64.npz"), H=H, llrs=llr64, iters=5,
+                        batch_size=48, clamp=10, out=out, out_dtype=str(out.dtype))
+
+    # 802.11n (648,1/2) through the reference algorithm (the reference accepts any binary H)
+    qc = wifi_code(648, "1/2")
+    Hw = qc.H()
+    enc = Encoder(Hw)
+    recs = {}
+    for snr in (1.0, 2.0):
+        rng = np.random.default_rng(648 + int(snr))
+        info = rng.integers(0, 2, size=(16, qc.k))
+        cw = enc.encode(info)
+        llr = bpsk_awgn_llr(cw.astype(np.float64), snr, 0.5, rng)
+        p1_32, _ = run_ref(Hw, 5, 10, llr)
+        p1_64, _ = run_ref(Hw, 5, 10, llr, double=True)
+        tag = f"snr{int(snr)}"
+        recs[f"llr_{tag}"] = llr
+        recs[f"codeword_{tag}"] = cw
+        recs[f"p1_f32_{tag}"] = p1_32.astype(np.float32)
+        recs[f"p1_f64_{tag}"] = p1_64
+        print("wifi648", tag, "bit errors:", int((np.round(p1_32) != cw).sum()))
+    np.savez_compressed(os.path.join(HERE, "bp_wifi648.npz"), base=qc.base, Z=qc.Z, iters=5, clamp=10,
+                        **recs)
+
+    # channel front end: the reference's LLR demodulator on a fixed received vector
+    rng = np.random.default_rng(5)
+    rx = (rng.standard_normal(64) + 1j * rng.standard_normal(64)) * 0.8
+    llrs, rsym = OF.demodulate_signal(rx.reshape(1, -1), 32, 10 ** (3.0 / 10))
+    np.savez_compressed(os.path.join(HERE, "demod_ofdm.npz"), rx=rx, snr_db=3.0, ofdm_size=32,
+                        llrs=llrs, rx_symbols=rsym)
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,60 @@
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from ldpc_amd.codes import Encoder, Graph, gf2_rank, peg_64_32, peg_64_32_generator, qc_expand, wifi_code
+
+
+def test_peg_matches_reference_fixture():
+    d = np.load(os.path.join(GOLDEN, "peg64_32.npz"))
+    assert np.array_equal(peg_64_32(), d["H"])
+    assert np.array_equal(peg_64_32_generator(), d["G"])
+
+
+def test_graph_numbering_is_reference_clookup_vlookup():
+    """masking.py:84-95: check-order ids = row-major nonzeros; var-order = column-major."""
+    H = peg_64_32()
+    g = Graph.from_H(H)
+    rows, cols = np.nonzero(H)
+    assert np.array_equal(g.col_idx, cols)
+    # var-order sequence of check-order ids == column-major enumeration of the nonzeros
+    rc = [(r, c) for r, c in zip(rows, cols)]
+    colmajor = sorted(range(len(rc)), key=lambda e: (rc[e][1], rc[e][0]))
+    assert np.array_equal(g.var_edges, colmajor)
+    assert g.E == 96 and g.m == 32 and g.n == 64
+
+
+@pytest.mark.parametrize("n,rate,Z,E,k", [(648, "1/2", 27, 2376, 324), (1296, "2/3", 54, 4752, 864),
+                                          (1944, "5/6", 81, 6399, 1620)])
+def test_wifi_tables_structure(n, rate, Z, E, k):
+    q = wifi_code(n, rate)
+    H = q.H()
+    assert q.Z == Z and q.n == n and q.k == k and int(H.sum()) == E
+    mb, nb = q.base.shape
+    kb = nb - mb
+    # dual-diagonal parity part: h_b column (x, ..., 0, ..., x) and identity staircase
+    hb = q.base[:, kb]
+    nz = np.nonzero(hb >= 0)[0]
+    assert len(nz) == 3 and nz[0] == 0 and nz[-1] == mb - 1 and hb[0] == hb[-1] and hb[nz[1]] == 0
+    for r in range(mb):
+        for j in range(kb + 1, nb):
+            c = j - kb - 1
+            assert (q.base[r, j] == 0) == (r in (c, c + 1)) and (q.base[r, j] in (-1, 0))
+    assert gf2_rank(H) == mb * Z
+    enc = Encoder(H)
+    info = np.random.default_rng(1).integers(0, 2, size=(8, enc.k))
+    cw = enc.encode(info)
+    assert np.array_equal(cw[:, :enc.k], info)
+    assert not ((H @ cw.T.astype(np.int64)) % 2).any()
+
+
+def test_qc_expand_shift_convention():
+    H = qc_expand(np.array([[1]]), 4)
+    assert H[0, 1] == 1 and H[3, 0] == 1 and H.sum() == 4
+
+
+def test_graph_rejects_non_binary():
+    with pytest.raises(ValueError):
+        Graph.from_H(np.array([[0, 2]]))

@@ -1,0 +1,171 @@
+"""GPU parity: the HIP decoder (through libldpc_hip.so's C ABI) against the reference's golden vectors and
+the CPU oracle.  Tolerances are stated per test; hard decisions must match exactly."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import ldpc_amd  # noqa: E402
+from ldpc_amd import _abi  # noqa: E402
+from ldpc_amd.codes import Encoder, get_code  # noqa: E402
+
+PEG_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_peg64_snr*.npz")))
+# GPU tanhf/logf/expf (ocml) differ from glibc/torch by ulps; near |p| -> 1 the reference's own
+# log((1+p)/(1-p)) amplifies that (its fp32 output is 2.2e-5 from its fp64 output on these files).
+TOL_P1_F32_VS_REF = 2e-5
+TOL_P1_F64_VS_REF = 1e-10
+
+
+def _llr(H, B, snr_db, seed, rate=0.5):
+    rng = np.random.default_rng(seed)
+    enc = Encoder(H)
+    cw = enc.encode(rng.integers(0, 2, size=(B, enc.k)))
+    sigma = np.sqrt(1.0 / (2 * rate * 10 ** (snr_db / 10)))
+    y = (1.0 - 2.0 * cw) + sigma * rng.standard_normal(cw.shape)
+    return cw, (-2.0 * y / sigma**2).astype(np.float32)
+
+
+@pytest.fixture(scope="module", params=[False, True], ids=["auto", "generic"])
+def force_generic(request):
+    return request.param
+
+
+@pytest.mark.parametrize("path", PEG_FILES, ids=lambda p: os.path.basename(p))
+def test_sp_f32_matches_reference_golden(path):
+    d = np.load(path)
+    dec = ldpc_amd.get_decoder(d["H"])
+    r = dec.decode(torch.from_numpy(d["llr"]).cuda(), int(d["iters"]), algo="tanh", clamp=float(d["clamp"]), soft="p1")
+    assert np.array_equal(r["bits"].cpu().numpy(), d["bits_f32"])
+    assert np.abs(r["soft"].cpu().numpy() - d["p1_f32"]).max() <= TOL_P1_F32_VS_REF
+
+
+@pytest.mark.parametrize("path", PEG_FILES, ids=lambda p: os.path.basename(p))
+def test_sp_f64_matches_reference_golden(path):
+    d = np.load(path)
+    dec = ldpc_amd.get_decoder(d["H"])
+    r = dec.decode(d["llr"].astype(np.float64), int(d["iters"]), algo="tanh", clamp=float(d["clamp"]),
+                   precision="f64", soft="p1")
+    assert np.array_equal(r["bits"], d["bits_f64"])
+    assert np.abs(r["soft"] - d["p1_f64"]).max() <= TOL_P1_F64_VS_REF
+
+
+def test_decode_bits_dropin_matches_reference_golden():
+    d = np.load(os.path.join(GOLDEN, "decode_bits_peg64.npz"))
+    out = ldpc_amd.decode_bits(d["llrs"], d["H"], int(d["iters"]), int(d["batch_size"]), int(d["clamp"]))
+    assert out.dtype == np.float64 and out.shape == d["out"].shape
+    assert np.array_equal(out, d["out"])
+    with pytest.raises(ZeroDivisionError):
+        ldpc_amd.decode_bits(d["llrs"], d["H"], 5, 0, 10)
+
+
+def test_belief_propagation_module_matches_reference_golden():
+    d = np.load(os.path.join(GOLDEN, "bp_peg64_snr2_it10_cl10.npz"))
+    BP = ldpc_amd.BeliefPropagation
+    m = BP(d["H"], 10).eval().cuda()
+    llr = torch.from_numpy(d["llr"]).cuda()
+    x = torch.zeros(llr.shape[0], m.layer_size(), device="cuda")
+    assert m.layer_size() == 96
+    p1 = m(x, llr, 10).cpu().numpy()
+    assert np.abs(p1 - d["p1_f32"]).max() <= TOL_P1_F32_VS_REF
+    m64 = m.double()
+    p64 = m64(x.double(), llr.double(), 10).cpu().numpy()
+    assert np.abs(p64 - d["p1_f64"]).max() <= TOL_P1_F64_VS_REF
+
+
+def test_wifi648_sp_matches_reference_golden(force_generic):
+    from ldpc_amd.codes import qc_expand
+    d = np.load(os.path.join(GOLDEN, "bp_wifi648.npz"))
+    H = qc_expand(d["base"], int(d["Z"]))
+    dec = ldpc_amd.get_decoder(H)
+    for tag in ("snr1", "snr2"):
+        r = dec.decode(d[f"llr_{tag}"], 5, algo="tanh", clamp=10.0, soft="p1", force_generic=force_generic)
+        assert np.array_equal(r["bits"], np.round(d[f"p1_f32_{tag}"]).astype(np.uint8))
+        assert np.abs(r["soft"] - d[f"p1_f32_{tag}"]).max() <= TOL_P1_F32_VS_REF
+        r = dec.decode(d[f"llr_{tag}"].astype(np.float64), 5, algo="tanh", clamp=10.0, soft="p1", precision="f64",
+                       force_generic=force_generic)
+        assert np.abs(r["soft"] - d[f"p1_f64_{tag}"]).max() <= TOL_P1_F64_VS_REF
+
+
+CODES = ["peg64_32", "wifi648_12", "wifi1296_23", "wifi1944_56"]
+
+
+@pytest.mark.parametrize("code", CODES)
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.8125, 0.0), (1.0, 0.5)])
+def test_minsum_bit_exact_vs_oracle(code, alpha, beta, force_generic):
+    """min-sum is compare/add only: GPU and oracle must agree bit for bit, soft (z) included."""
+    H, qc = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, 1000, 2.0 if rate < 0.6 else 4.0, seed=11, rate=rate)
+    llr[0] = 0.0                       # all-zero codeword LLRs: ties everywhere
+    llr[1, ::3] = 0.0
+    llr[2] = np.float32(1e30)         # saturating magnitudes
+    dec = ldpc_amd.get_decoder(H)
+    r = dec.decode(torch.from_numpy(llr).cuda(), 25, algo="minsum", clamp=20.0, alpha=alpha, beta=beta, soft="z",
+                   force_generic=force_generic)
+    ref = oracle.ms_f32(H, llr, 25, 20.0, alpha, beta)
+    assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])
+    assert np.array_equal(r["soft"].cpu().numpy().view(np.uint32), ref["z"].view(np.uint32))
+
+
+@pytest.mark.parametrize("code", CODES)
+def test_sp_hard_bits_vs_oracle(code, force_generic):
+    H, _ = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, 512, 1.5 if rate < 0.6 else 3.5, seed=12, rate=rate)
+    dec = ldpc_amd.get_decoder(H)
+    r = dec.decode(llr, 8, algo="tanh", clamp=10.0, soft="z", force_generic=force_generic)
+    ref = oracle.sp_f32(H, llr, 8, 10.0)
+    mism = int((r["bits"] != ref["bits"]).sum())
+    assert mism == 0, f"{mism} hard-bit mismatches"
+    # soft: half-LLR z; ulp-level transcendental differences, amplified near saturation
+    assert np.abs(r["soft"] - ref["z"]).max() <= 2e-3 * max(1.0, np.abs(ref["z"]).max() / 100)
+
+
+@pytest.mark.parametrize("B", [1, 63, 64, 65, 1000])
+def test_ragged_batches(B):
+    H, _ = get_code("wifi648_12")
+    cw, llr = _llr(H, B, 2.0, seed=B)
+    dec = ldpc_amd.get_decoder(H)
+    r = dec.decode(llr, 10, algo="minsum", clamp=20.0, soft="z")
+    ref = oracle.ms_f32(H, llr, 10, 20.0)
+    assert np.array_equal(r["bits"], ref["bits"]) and np.array_equal(r["soft"], ref["z"])
+
+
+def test_zero_iterations_and_empty_batch():
+    H, _ = get_code("peg64_32")
+    cw, llr = _llr(H, 16, 2.0, seed=3)
+    dec = ldpc_amd.get_decoder(H)
+    r = dec.decode(llr, 0, algo="tanh", clamp=10.0, soft="z")
+    assert np.array_equal(r["soft"], (np.float32(0.5) * -llr).astype(np.float32))
+    r = dec.decode(np.zeros((0, 64), np.float32), 5)
+    assert r["bits"].shape == (0, 64)
+
+
+def test_count_errors_and_awgn():
+    lib = _abi.load()
+    B, n = 3000, 648
+    bits = torch.randint(0, 2, (B, n), dtype=torch.uint8, device="cuda")
+    ref = torch.randint(0, 2, (B, n), dtype=torch.uint8, device="cuda")
+    ref[:100] = bits[:100]
+    counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    _abi.check(lib.ldpc_count_errors(bits.data_ptr(), ref.data_ptr(), B, n, 324, counts.data_ptr(), st))
+    b, r = bits.cpu().numpy(), ref.cpu().numpy()
+    assert counts.cpu().tolist() == [int((b[:, :324] != r[:, :324]).sum()), int((b != r).any(1).sum()), B]
+    llr = torch.empty((B, n), dtype=torch.float32, device="cuda")
+    sigma = 0.8
+    _abi.check(lib.ldpc_awgn_llr(ref.data_ptr(), llr.data_ptr(), B, n, sigma, 1234, 0, st))
+    y = (-llr * sigma**2 / 2).cpu().numpy()
+    noise = y - (1 - 2 * r.astype(np.float64))
+    assert abs(noise.mean()) < 0.01 and abs(noise.std() - sigma) < 0.01
+    # a shard's LLRs do not depend on the shard split
+    llr2 = torch.empty((B - 1000, n), dtype=torch.float32, device="cuda")
+    _abi.check(lib.ldpc_awgn_llr(ref[1000:].data_ptr(), llr2.data_ptr(), B - 1000, n, sigma, 1234, 1000, st))
+    assert torch.equal(llr2, llr[1000:])

@@ -1,0 +1,54 @@
+"""Min-sum / quantized min-sum oracle: no reference counterpart ("parity unpinned"), so it
+is pinned by an independent numpy restatement (bit-exact) and by decoding properties."""
+import numpy as np
+import pytest
+
+import oracle
+import numpy_ref
+from ldpc_amd.codes import Encoder, get_code
+
+
+def _llr(H, B, snr_db, seed, rate=0.5):
+    rng = np.random.default_rng(seed)
+    enc = Encoder(H)
+    cw = enc.encode(rng.integers(0, 2, size=(B, enc.k)))
+    sigma = np.sqrt(1.0 / (2 * rate * 10 ** (snr_db / 10)))
+    y = (1.0 - 2.0 * cw) + sigma * rng.standard_normal(cw.shape)
+    return cw, (-2.0 * y / sigma**2).astype(np.float32)
+
+
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.75, 0.0), (1.0, 0.25)])
+def test_ms_oracle_equals_numpy_restatement(alpha, beta):
+    H, _ = get_code("peg64_32")
+    cw, llr = _llr(H, 64, 1.0, 3)
+    llr[0, :5] = 0.0      # ties / zero-magnitude messages
+    llr[1, :] = 0.0
+    r = oracle.ms_f32(H, llr, 7, 20.0, alpha, beta)
+    z = numpy_ref.ms(H, llr, 7, 20.0, alpha, beta)
+    assert np.array_equal(r["z"].view(np.uint32), z.astype(np.float32).view(np.uint32))
+
+
+def test_ms_decodes_at_high_snr():
+    H, _ = get_code("wifi648_12")
+    cw, llr = _llr(H, 64, 4.0, 5)
+    r = oracle.ms_f32(H, llr, 20, 20.0)
+    assert (r["bits"] != cw).sum() == 0
+
+
+def test_ms_early_stop_counts_iterations():
+    H, _ = get_code("wifi648_12")
+    cw, llr = _llr(H, 64, 4.0, 6)
+    full = oracle.ms_f32(H, llr, 20, 20.0)
+    es = oracle.ms_f32(H, llr, 20, 20.0, early_stop=True)
+    assert (es["iters_used"] < 20).all() and (es["iters_used"] >= 1).all()
+    assert np.array_equal(es["bits"], cw)
+    assert (full["iters_used"] == 20).all()
+
+
+def test_qms_oracle_decodes():
+    H, _ = get_code("wifi1296_23")
+    cw, llr = _llr(H, 32, 4.0, 8, rate=2 / 3)
+    q = np.clip(np.rint(llr / 1.0), -15, 15).astype(np.int8)
+    r = oracle.qms(H, q, 20, 15, 127, 0, early_stop=True)
+    assert (r["bits"] != cw).sum() == 0
+    assert (r["iters_used"] <= 20).all()

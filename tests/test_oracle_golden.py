@@ -1,0 +1,86 @@
+"""Pin the CPU oracle against the reference's own outputs (tests/golden, made by make_golden.py from
+pytorch/bp/bp.py + ofdm_functions.decode_bits run in the build container)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import numpy_ref
+from conftest import GOLDEN
+
+PEG_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_peg64_snr*.npz")))
+
+# tolerances (documented in DESIGN.md "Parity"): fp32 soft output p1 vs the reference's fp32 module;
+# fp64 vs the reference module after .double().
+TOL_P1_F32 = 5e-6
+TOL_P1_F64 = 1e-12
+
+
+def test_golden_files_present():
+    assert len(PEG_FILES) == 15
+
+
+@pytest.mark.parametrize("path", PEG_FILES, ids=lambda p: os.path.basename(p))
+def test_oracle_sp_f32_matches_reference(path):
+    d = np.load(path)
+    r = oracle.sp_f32(d["H"], d["llr"], int(d["iters"]), float(d["clamp"]))
+    assert np.array_equal(r["bits"], d["bits_f32"])
+    assert np.abs(r["p1"] - d["p1_f32"]).max() <= TOL_P1_F32
+
+
+@pytest.mark.parametrize("path", PEG_FILES, ids=lambda p: os.path.basename(p))
+def test_oracle_sp_f64_matches_reference(path):
+    d = np.load(path)
+    r = oracle.sp_f64(d["H"], d["llr"].astype(np.float64), int(d["iters"]), float(d["clamp"]))
+    assert np.array_equal(r["bits"], d["bits_f64"])
+    assert np.abs(r["p1"] - d["p1_f64"]).max() <= TOL_P1_F64
+
+
+def test_oracle_c2v_trace_matches_reference():
+    """Per-iteration check-order messages x (bp/bp.py:46-47): pins edge numbering and the CV update."""
+    d = np.load(os.path.join(GOLDEN, "bp_peg64_trace.npz"))
+    r = oracle.sp_f32(d["H"], d["llr"], 5, 10.0, trace=True)
+    assert r["trace"].shape == d["x_f32"].shape
+    assert np.abs(r["trace"] - d["x_f32"]).max() <= 2e-5   # c2v values are up to 16.6: ~1 ulp-level
+    # in fp64 the restatement follows the reference to rounding
+    z64 = numpy_ref.sp(d["H"], d["llr"].astype(np.float64), 5, 10.0)
+    p1 = 1 - 1 / (1 + np.exp(-z64))
+    assert np.abs(p1 - d["p1_f64"]).max() <= 1e-12
+
+
+def test_oracle_decode_bits_boundary():
+    """decode_bits (ofdm_functions.py:131-163): float64 output, ragged tail rows stay 0."""
+    d = np.load(os.path.join(GOLDEN, "decode_bits_peg64.npz"))
+    out = d["out"]
+    assert str(d["out_dtype"]) == "float64"
+    N, bs = out.shape[0], int(d["batch_size"])
+    rows = (N // bs) * bs
+    r = oracle.sp_f32(d["H"], d["llrs"].astype(np.float32), int(d["iters"]), float(d["clamp"]))
+    assert np.array_equal(r["bits"][:rows].astype(np.float64), out[:rows])
+    assert not out[rows:].any()
+
+
+def test_oracle_wifi648_matches_reference():
+    from ldpc_amd.codes import qc_expand
+    d = np.load(os.path.join(GOLDEN, "bp_wifi648.npz"))
+    H = qc_expand(d["base"], int(d["Z"]))
+    for tag in ("snr1", "snr2"):
+        r32 = oracle.sp_f32(H, d[f"llr_{tag}"], 5, 10.0)
+        r64 = oracle.sp_f64(H, d[f"llr_{tag}"].astype(np.float64), 5, 10.0)
+        assert np.array_equal(r32["bits"], np.round(d[f"p1_f32_{tag}"]).astype(np.uint8))
+        assert np.array_equal(r64["bits"], np.round(d[f"p1_f64_{tag}"]).astype(np.uint8))
+        assert np.abs(r32["p1"] - d[f"p1_f32_{tag}"]).max() <= TOL_P1_F32
+        assert np.abs(r64["p1"] - d[f"p1_f64_{tag}"]).max() <= TOL_P1_F64
+
+
+def test_hard_decision_threshold():
+    """bit = np.round(1 - sigmoid(z)) in fp32 <=> z <= -1.7881392e-07 (0xb43fffff), measured on torch 2.10."""
+    thr = np.array([0xB43FFFFF], np.uint32).view(np.float32)[0]
+    assert thr == np.float32(-1.7881392e-07)
+    H = np.array([[1, 1]])
+    # iters=0: z = -0.5*llr, so llr = -2z probes the decision directly
+    zs = np.array([[thr, thr], [np.nextafter(thr, np.float32(0)), 0.0]], np.float32)
+    r = oracle.sp_f32(H, (-2 * zs).astype(np.float32), 0, 10.0)
+    assert r["bits"].tolist() == [[1, 1], [0, 0]]

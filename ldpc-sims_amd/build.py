@@ -9,6 +9,7 @@ SRCS = ["abi.hip", "generic.hip", "qc.hip"]
 OUT = os.path.join(HERE, "ldpc_amd", "libldpc_hip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off",  # min-sum must round exactly like oracle/ldpc_oracle.c (no FMA contraction)
+         "-fno-slp-vectorize",  # v_pk_* f32 pairs need aligned register pairs: +100 VGPRs in the QC kernel
          "-Wall", "-Wno-unused-function"]
 
 
@@ -16,6 +17,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     srcs = [os.path.join(HERE, "csrc", s) for s in SRCS]
     deps = srcs + [os.path.join(HERE, "csrc", "common.h"), os.path.join(ROOT, "include", "ldpc_abi.h")]
     deps += [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
+    deps.append(os.path.abspath(__file__))
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps):
         return OUT
     cmd = ["hipcc", *FLAGS, "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc"), "-o", OUT, *srcs]

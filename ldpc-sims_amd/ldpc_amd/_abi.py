@@ -46,6 +46,13 @@ def load(path: str | None = None):
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
+    try:
+        # torch ships its own libamdhip64.so (soname libamdhip64.so.7).  Loading torch first makes our
+        # DT_NEEDED libamdhip64.so.7 resolve to that same runtime instead of a second copy from /opt/rocm
+        # (two HIP runtimes in one process see different device sets).
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(p):
         raise ImportError(f"{p} not found: the HIP decoder is not built (run `python __graft_entry__.py`); "
                           "there is no CPU fallback")

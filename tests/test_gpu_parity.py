@@ -169,3 +169,47 @@ def test_count_errors_and_awgn():
     llr2 = torch.empty((B - 1000, n), dtype=torch.float32, device="cuda")
     _abi.check(lib.ldpc_awgn_llr(ref[1000:].data_ptr(), llr2.data_ptr(), B - 1000, n, sigma, 1234, 1000, st))
     assert torch.equal(llr2, llr[1000:])
+
+
+# ---------------------------------------------------------------- QC register kernel specifics
+QC_CODES = ["wifi648_12", "wifi1296_23"]
+
+
+@pytest.mark.parametrize("code", QC_CODES)
+def test_qc_kernel_is_selected(code):
+    H, qc = get_code(code)
+    assert ldpc_amd.get_decoder(H).qc_z == qc.Z
+
+
+@pytest.mark.parametrize("code", QC_CODES)
+@pytest.mark.parametrize("snr", [1.0, 2.5, 4.0])
+def test_qc_early_stop_vs_oracle(code, snr):
+    H, qc = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, 777, snr + (2.0 if rate > 0.6 else 0.0), seed=int(snr * 10), rate=rate)
+    dec = ldpc_amd.get_decoder(H)
+    r = dec.decode(torch.from_numpy(llr).cuda(), 20, algo="minsum", clamp=20.0, alpha=0.8125, early_stop=True,
+                   soft="z", want_iters=True)
+    ref = oracle.ms_f32(H, llr, 20, 20.0, 0.8125, 0.0, early_stop=True)
+    assert np.array_equal(r["iters_used"].cpu().numpy(), ref["iters_used"])
+    assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])
+    assert np.array_equal(r["soft"].cpu().numpy().view(np.uint32), ref["z"].view(np.uint32))
+
+
+@pytest.mark.parametrize("code", QC_CODES)
+@pytest.mark.parametrize("early", [False, True])
+@pytest.mark.parametrize("beta", [0, 1])
+def test_qc_quantized_minsum_vs_oracle(code, early, beta):
+    H, qc = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, 500, 3.0 if rate < 0.6 else 4.5, seed=21 + beta, rate=rate)
+    qstep = np.float32(0.75)
+    qinv = np.float32(1.0) / qstep
+    q = np.clip(np.rint(llr * qinv), -15, 15).astype(np.int8)
+    dec = ldpc_amd.get_decoder(H)
+    r = dec.decode(llr, 20, algo="qminsum", qmax=15, app_max=127, qstep=float(qstep), beta=float(beta),
+                   early_stop=early, soft="z", want_iters=True)
+    ref = oracle.qms(H, q, 20, 15, 127, beta, early_stop=early)
+    assert np.array_equal(r["iters_used"], ref["iters_used"])
+    assert np.array_equal(r["bits"], ref["bits"])
+    assert np.array_equal(r["soft"], (0.5 * ref["app"]).astype(np.float32))

@@ -56,6 +56,7 @@ def main():
     import ldpc_amd
     from ldpc_amd import _abi
     from ldpc_amd.codes import Encoder
+    from ldpc_amd.dist import allreduce_counts, max_over_ranks
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -103,8 +104,7 @@ def main():
     for i in range(len(ebn0)):
         step(llrs[i])
         _abi.check(lib.ldpc_count_errors(bits.data_ptr(), cw.data_ptr(), B, n, k, counts[i].data_ptr(), st))
-    if world > 1:
-        dist.all_reduce(counts)  # the one collective: per-point error counters, 24 B x 11 per rank
+    allreduce_counts(counts)  # the one collective: per-point error counters, 24 B x 11 per rank (RCCL)
     c = counts.cpu().numpy().astype(np.float64)
     coded_ber = (c[:, 0] / (c[:, 2] * k)).tolist()
     coded_bler = (c[:, 1] / c[:, 2]).tolist()
@@ -129,10 +129,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     gpu_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(elapsed, device="cuda")
     total_cw = world * args.steps * B
     value = total_cw / elapsed
 

@@ -24,6 +24,15 @@
 
 namespace ldpc {
 
+#ifndef QC_ADDR_SGPR_MASK
+#define QC_ADDR_SGPR_MASK 1  // rotation-address select with a compile-time lane mask (1 VALU, no v_cmp)
+#endif
+#ifndef QC_ID_AT_VN
+#define QC_ID_AT_VN 1  // find the min slot by |v| == min1 at VN time instead of tracking it in CN
+#endif
+#ifndef QC_ROW_BARRIER
+#define QC_ROW_BARRIER 0  // measured +1.9% without the per-row scheduling barrier
+#endif
 #ifndef QC_WAVES_PER_SIMD
 #define QC_WAVES_PER_SIMD 4  // 128 VGPRs: 16 waves (32 codewords at Z=27) resident per CU
 #endif
@@ -60,6 +69,26 @@ constexpr int first_slot(int r, int j) {
     for (int t = 0; t < C::DEG[r]; ++t)
         if (C::COL[r][t] == j) return t;
     return -1;
+}
+
+// lanes whose lifting index z lies in [lo, hi), in each codeword's lane group
+template <int Z, int CPW>
+constexpr uint64_t lane_range_mask(int lo, int hi) {
+    uint64_t m = 0;
+    for (int z = lo; z < hi; ++z) {
+        m |= 1ull << z;
+        if (CPW == 2) m |= 1ull << (32 + z);
+    }
+    return m;
+}
+
+// lane in MASK ? b : a.  The mask is a compile-time SGPR-pair constant, so the select is one VALU op
+// with no v_cmp (and no VCC hazard).  Volatile: never CSE'd across rows or hoisted out of the loop.
+template <uint64_t MASK>
+__device__ __forceinline__ int sel_lanes(int a, int b) {
+    int r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(MASK));
+    return r;
 }
 
 __device__ __forceinline__ float bperm(int addr, float v) {
@@ -129,7 +158,9 @@ __global__ __launch_bounds__(256, QC_WAVES_PER_SIMD) void k_qc_ms(const float* _
             // Row boundary: fresh (opaque) lane constants stop GVN/LICM from keeping equal-shift rotation
             // addresses of different rows (and iterations) alive; the scheduling barrier keeps those
             // copies inside their row instead of at the loop head.
+#if QC_ROW_BARRIER
             __builtin_amdgcn_sched_barrier(0);
+#endif
             int zr = z, br = base4, bmr = base4m, lr = lbase;
             asm volatile("" : "+v"(zr), "+v"(br), "+v"(bmr), "+v"(lr));
             static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
@@ -148,7 +179,11 @@ __global__ __launch_bounds__(256, QC_WAVES_PER_SIMD) void k_qc_ms(const float* _
                 if constexpr (s == 0) {
                     a = app[j];
                 } else {
+#if QC_ADDR_SGPR_MASK
+                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(br, bmr) + 4 * s;
+#else
                     const int addr = ((zr >= Z - s) ? bmr : br) + 4 * s;
+#endif
                     a = bperm(addr, app[j]);
                 }
                 // hard bit(APP) = APP <= thr2 <=> APP - thr2n < 0, thr2n = next float above thr2: a
@@ -160,7 +195,9 @@ __global__ __launch_bounds__(256, QC_WAVES_PER_SIMD) void k_qc_ms(const float* _
                 if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
                 v[t] = x;
                 const float m = fabsf(x);
+#if !QC_ID_AT_VN
                 id = (m < mn1) ? (uint32_t)t : id;
+#endif
                 mn2 = __builtin_amdgcn_fmed3f(mn1, m, mn2);
                 mn1 = fminf(mn1, m);
                 tot ^= __float_as_uint(x);
@@ -173,14 +210,26 @@ __global__ __launch_bounds__(256, QC_WAVES_PER_SIMD) void k_qc_ms(const float* _
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int j = C::COL[r][t], s = C::SH[r][t];
+#if QC_ID_AT_VN
+                // the min slot is the one with |v| == min1; if several tie, min2 == min1 and M2 == M1,
+                // so the choice (and the stored argmin) cannot change any value: bit-exact vs the oracle
+                const bool ismin = fabsf(v[t]) == mn1;
+                const float mg = ismin ? M2 : M1;
+                id = ismin ? (uint32_t)t : id;
+#else
                 const float mg = (id == (uint32_t)t) ? M2 : M1;
+#endif
                 const float c = __uint_as_float(__float_as_uint(mg) | ((tot ^ __float_as_uint(v[t])) & 0x80000000u));
                 sg = __builtin_amdgcn_alignbit(sg, __float_as_uint(c), 31);
                 float cr;
                 if constexpr (s == 0) {
                     cr = c;
                 } else {
+#if QC_ADDR_SGPR_MASK
+                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(br, bmr) + 4 * (Z - s);
+#else
                     const int addr = ((zr >= s) ? bmr : br) + 4 * (Z - s);
+#endif
                     cr = bperm(addr, c);
                 }
                 nap[j] = nap[j] + cr;

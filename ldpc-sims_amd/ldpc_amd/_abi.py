@@ -45,7 +45,8 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # LDPC_LIB: alternative build of the same library (used to A/B kernel variants in one GPU session)
+    p = path or os.environ.get("LDPC_LIB") or LIB_PATH
     try:
         # torch ships its own libamdhip64.so (soname libamdhip64.so.7).  Loading torch first makes our
         # DT_NEEDED libamdhip64.so.7 resolve to that same runtime instead of a second copy from /opt/rocm

@@ -61,9 +61,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LDPC_BENCH_BACKEND / device modulo exist only to rehearse N>1 on a 1-GPU box (ranks share cuda:0,
+    # counters over gloo); the driver's multi-GPU runs use the defaults: one GPU per rank, RCCL.
+    local = local % max(1, torch.cuda.device_count()) if os.environ.get("LDPC_BENCH_SHARE_GPU") else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))  # RCCL over xGMI
+        backend = os.environ.get("LDPC_BENCH_BACKEND", "nccl")  # nccl == RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     H, qc = ldpc_amd.get_code(args.code)
     m, n = H.shape

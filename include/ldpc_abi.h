@@ -107,6 +107,10 @@ int ldpc_count_errors(const uint8_t* bits, const uint8_t* ref, int64_t B, int32_
 int ldpc_awgn_llr(const uint8_t* codeword, float* llr, int64_t B, int32_t n, float sigma, uint64_t seed,
                   int64_t b0, void* stream);
 
+/* Uniform random information bits on device: out[b][i] = bit of Philox(key = seed, counter = (b0+b)*k + i),
+ * so the bits of global codeword b0+b do not depend on how a sweep is sharded.  out: device uint8 [B][k]. */
+int ldpc_random_bits(uint8_t* out, int64_t B, int32_t k, uint64_t seed, int64_t b0, void* stream);
+
 const char* ldpc_last_error(void);
 int ldpc_device_count(void);
 const char* ldpc_version(void);

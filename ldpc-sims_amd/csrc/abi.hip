@@ -110,6 +110,15 @@ __global__ __launch_bounds__(256) void k_awgn(const uint8_t* __restrict__ cw, fl
     }
 }
 
+__global__ __launch_bounds__(256) void k_random_bits(uint8_t* __restrict__ out, int64_t B, int k, uint64_t seed,
+                                                     int64_t b0) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * k) return;
+    uint32_t r[4];
+    Philox::gen((uint64_t)(b0 * k + i), seed ^ 0x9E3779B97F4A7C15ull, r);
+    out[i] = (uint8_t)(r[0] & 1u);
+}
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -410,6 +419,15 @@ int ldpc_awgn_llr(const uint8_t* codeword, float* llr, int64_t B, int32_t n, flo
     k_awgn<<<(unsigned)((quads + 255) / 256), 256, 0, (hipStream_t)stream>>>(codeword, llr, B, n, sigma, seed, b0);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "awgn: %s", hipGetErrorString(e));
+    return LDPC_OK;
+}
+
+int ldpc_random_bits(uint8_t* out, int64_t B, int32_t k, uint64_t seed, int64_t b0, void* stream) {
+    if (!out || B < 0 || k <= 0 || b0 < 0) return set_error(LDPC_EINVAL, "bad random_bits arguments");
+    if (B == 0) return LDPC_OK;
+    k_random_bits<<<(unsigned)((B * k + 255) / 256), 256, 0, (hipStream_t)stream>>>(out, B, k, seed, b0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(LDPC_EHIP, "random_bits: %s", hipGetErrorString(e));
     return LDPC_OK;
 }
 

@@ -47,11 +47,22 @@ class SweepResult:
         return (self.counts[:, 1] / np.maximum(self.counts[:, 2], 1)).tolist()
 
 
+def _backend_device_ok(t, group):
+    import torch.distributed as dist
+    # gloo reduces CPU tensors only: stage through host when the counters live on the GPU
+    return not (t.is_cuda and dist.get_backend(group) == "gloo")
+
+
 def allreduce_counts(counts, group=None):
     """Sum the per-point error counters over ranks (the only collective)."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        if _backend_device_ok(counts, group):
+            dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+        else:
+            h = counts.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            counts.copy_(h)
     return counts
 
 
@@ -60,6 +71,8 @@ def max_over_ranks(value: float, device="cpu", group=None) -> float:
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         t = torch.tensor([value], dtype=torch.float64, device=device)
+        if not _backend_device_ok(t, group):
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         return float(t.item())
     return value

@@ -1,0 +1,140 @@
+"""BER/BLER-vs-Eb/N0 sweep on the GPU, with the reference evaluators' metrics.
+
+Reproduces what ``evaluate_quantized.py`` / ``evaluate_snr.py`` compute around ``decode_bits``
+(``evaluate_quantized.py:83-149``): for each SNR point, random information bits, systematic encoding,
+channel, LLRs, decode, then
+  * uncoded BER  = mean(|sign-decision(llr) - codeword|) over all n bits   (``:139``; cbits = (sign+1)//2)
+  * coded BER    = mean(|bits[:, :k] - codeword[:, :k]|) over the information bits (``:140``)
+  * coded BLER   = fraction of codewords with any error over all n bits      (``:141``)
+The channel is BPSK/AWGN generated on device (``ldpc_awgn_llr``), distributionally identical to the
+reference's QPSK over unitary-DFT OFDM at SNR(dB) = Eb/N0(dB) for rate 1/2.
+Results can be written in the reference's ``outputs/ber/*.pkl`` key schema so ``plots.py`` reads them.
+
+    python -m ldpc_amd.sweep --code peg64_32 --algo tanh --iters 3 --clamp 20 --snr 0:1:10 --n 65536
+    torchrun --nproc-per-node 8 -m ldpc_amd.sweep ...        # shards codewords; one RCCL all-reduce
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pickle
+import time
+
+import numpy as np
+
+from . import _abi
+from .api import get_decoder
+from .codes import Encoder, get_code
+from .dist import ebn0_sigma, sweep as dist_sweep
+
+
+def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=0.0, snr_db=(0.0,),
+        codewords=65536, batch=65536, seed=1, rank=0, world=1, device=0, early_stop=False, qstep=1.0,
+        qmax=15, app_max=127):
+    """Returns dict(snrdb, uncoded_ber, coded_ber, coded_bler, codewords, seconds)."""
+    import torch
+    H, _ = get_code(code) if isinstance(code, str) else (np.asarray(code), None)
+    m, n = H.shape
+    k = n - m
+    rate = k / n
+    dec = get_decoder(H, device)
+    lib = _abi.load()
+    enc = Encoder(H)
+    dev = torch.device("cuda", device)
+    Gp = torch.from_numpy(enc.generator_parity().astype(np.float32)).to(dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    p = dec.params(iters, algo, clamp, alpha, beta, early_stop, "f32", "p1", qmax, app_max, qstep,
+                   device_ptrs=True)
+    bmax = min(batch, codewords)
+    wsb = dec.workspace_bytes(bmax, p)
+    ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dev)
+    info = torch.empty((bmax, k), dtype=torch.uint8, device=dev)
+    llr = torch.empty((bmax, n), dtype=torch.float32, device=dev)
+    bits = torch.empty((bmax, n), dtype=torch.uint8, device=dev)
+    unc = torch.zeros((len(snr_db),), dtype=torch.int64, device=dev)
+
+    def run_shard(i, lo, hi, sigma):
+        cnt = torch.zeros(3, dtype=torch.int64, device=dev)
+        for s in range(lo, hi, bmax):
+            B = min(bmax, hi - s)
+            _abi.check(lib.ldpc_random_bits(info.data_ptr(), B, k, seed * 7919 + i, s, st))
+            par = torch.remainder(info[:B].float() @ Gp, 2.0).to(torch.uint8)
+            cw = torch.cat([info[:B], par], dim=1).contiguous()
+            _abi.check(lib.ldpc_awgn_llr(cw.data_ptr(), llr.data_ptr(), B, n, sigma, seed * 104729 + i, s, st))
+            unc[i] += ((llr[:B] > 0).to(torch.uint8) != cw).sum()      # (np.sign(llr)+1)//2 decisions
+            _abi.check(lib.ldpc_decode_ex(dec._h, llr.data_ptr(), B, p, bits.data_ptr(), None, None,
+                                          ws.data_ptr(), wsb, st))
+            _abi.check(lib.ldpc_count_errors(bits.data_ptr(), cw.data_ptr(), B, n, k, cnt.data_ptr(), st))
+        return cnt.cpu().numpy()
+
+    t0 = time.perf_counter()
+    res = dist_sweep(list(snr_db), codewords, rate, k, run_shard, rank=rank, world=world, device=dev)
+    from .dist import allreduce_counts
+    allreduce_counts(unc)
+    secs = time.perf_counter() - t0
+    c = res.counts.astype(np.float64)
+    return dict(snrdb=np.asarray(snr_db, dtype=np.float64),
+                uncoded_ber=unc.cpu().numpy() / (c[:, 2] * n),
+                coded_ber=c[:, 0] / (c[:, 2] * k),
+                coded_bler=c[:, 1] / c[:, 2],
+                codewords=c[:, 2].astype(np.int64), seconds=secs,
+                config=dict(code=code if isinstance(code, str) else "custom", algo=algo, iters=iters,
+                            clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop))
+
+
+def save(result: dict, path: str):
+    """``.pkl``: the reference's schema (``evaluate_quantized.py:156-172`` keys snrdb, uncoded_ber,
+    coded_ber, coded_bler as numpy arrays) for plots.py; ``.json``: plain lists."""
+    if path.endswith(".pkl"):
+        keep = {kk: np.asarray(result[kk]) for kk in ("snrdb", "uncoded_ber", "coded_ber", "coded_bler")}
+        with open(path, "wb") as f:
+            pickle.dump(keep, f)
+    else:
+        with open(path, "w") as f:
+            json.dump({kk: (v.tolist() if isinstance(v, np.ndarray) else v) for kk, v in result.items()}, f, indent=1)
+
+
+def _parse_points(s):
+    lo, st, hi = (float(x) for x in s.split(":"))
+    return list(np.round(np.arange(lo, hi + 1e-9, st), 6))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--code", default="wifi648_12")
+    ap.add_argument("--algo", default="minsum")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--clamp", type=float, default=20.0)
+    ap.add_argument("--alpha", type=float, default=1.0)
+    ap.add_argument("--beta", type=float, default=0.0)
+    ap.add_argument("--snr", default="0:0.5:5")
+    ap.add_argument("--n", type=int, default=65536, help="codewords per SNR point (all ranks)")
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--early-stop", action="store_true")
+    ap.add_argument("--out", default=None, help="results .json or .pkl (reference schema)")
+    a = ap.parse_args(argv)
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    r = run(a.code, a.algo, a.iters, a.clamp, a.alpha, a.beta, _parse_points(a.snr), a.n, a.batch, a.seed,
+            rank, world, local, a.early_stop)
+    if rank == 0:
+        for i, e in enumerate(r["snrdb"]):
+            print(f"{e:5.2f} dB  uncoded {r['uncoded_ber'][i]:.4e}  coded BER {r['coded_ber'][i]:.4e}  "
+                  f"BLER {r['coded_bler'][i]:.4e}  ({r['codewords'][i]} cw)")
+        print(f"{r['seconds']:.2f} s")
+        if a.out:
+            save(r, a.out)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

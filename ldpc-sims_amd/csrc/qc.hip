@@ -34,7 +34,10 @@ namespace ldpc {
 #define QC_ROW_BARRIER 0  // measured +1.9% without the per-row scheduling barrier
 #endif
 #ifndef QC_WAVES_PER_SIMD
-#define QC_WAVES_PER_SIMD 4  // 128 VGPRs: 16 waves (32 codewords at Z=27) resident per CU
+#define QC_WAVES_PER_SIMD 5  // 96 VGPRs: 20 waves (40 codewords at Z=27) resident per CU
+#endif
+#ifndef QC_WAVES_PER_SIMD_EARLY
+#define QC_WAVES_PER_SIMD_EARLY 4  // early stop keeps APP_it live to the iteration end: 128 VGPRs
 #endif
 
 struct QCSpec {
@@ -91,14 +94,26 @@ __device__ __forceinline__ int sel_lanes(int a, int b) {
     return r;
 }
 
+// ms_mag (oracle: min(clamp, max(alpha*m - beta, 0))) specialised on which of alpha != 1 / beta != 0
+// hold: alpha == 1 makes alpha*m exact and beta == 0 makes max(m - 0, 0) == m for m >= 0 (m is a
+// minimum of |v|, never negative), so each form is bit-identical to the general one for its case.
+enum { NORM_PLAIN = 0, NORM_ALPHA = 1, NORM_BETA = 2, NORM_BOTH = 3 };
+template <int NORM>
+__device__ __forceinline__ float mag_of(float m, float alpha, float beta, float clamp) {
+    if constexpr (NORM == NORM_PLAIN) return fminf(m, clamp);
+    else if constexpr (NORM == NORM_ALPHA) return fminf(alpha * m, clamp);
+    else if constexpr (NORM == NORM_BETA) return fminf(fmaxf(m - beta, 0.0f), clamp);
+    else return ms_mag(m, alpha, beta, clamp);
+}
+
 __device__ __forceinline__ float bperm(int addr, float v) {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
 }
 
 // QUANT = false: float min-sum.  QUANT = true: integer offset min-sum carried in float registers (all
 // values are small integers, so every add/sub is exact and equals the oracle's int arithmetic).
-template <class C, bool QUANT, bool EARLY>
-__global__ __launch_bounds__(256, QC_WAVES_PER_SIMD) void k_qc_ms(const float* __restrict__ llr, int64_t B, int iters, float clamp,
+template <class C, bool QUANT, bool EARLY, int NORM>
+__global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER_SIMD) void k_qc_ms(const float* __restrict__ llr, int64_t B, int iters, float clamp,
                                                float alpha, float beta, float qmax, float app_max, float qinv,
                                                int flags, uint8_t* __restrict__ bits, float* __restrict__ soft,
                                                int32_t* __restrict__ iters_used) {
@@ -204,8 +219,8 @@ __global__ __launch_bounds__(256, QC_WAVES_PER_SIMD) void k_qc_ms(const float* _
             });
             if constexpr (early) unsat |= __ballot((int)par < 0);
             tot &= 0x80000000u;
-            const float M1 = ms_mag(mn1, alpha, beta, clamp);
-            const float M2 = ms_mag(mn2, alpha, beta, clamp);
+            const float M1 = mag_of<NORM>(mn1, alpha, beta, clamp);
+            const float M2 = mag_of<NORM>(mn2, alpha, beta, clamp);
             uint32_t sg = 0;
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
@@ -277,11 +292,22 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     float* sf = (float*)soft;
     if (p.algo == LDPC_ALGO_QMIN_SUM) {
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
-        if (es) k_qc_ms<C, true, true><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used);
-        else    k_qc_ms<C, true, false><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used);
+#define QL(E, N) k_qc_ms<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used)
+        if (b != 0.0f) { if (es) QL(true, NORM_BETA); else QL(false, NORM_BETA); }
+        else           { if (es) QL(true, NORM_PLAIN); else QL(false, NORM_PLAIN); }
+#undef QL
     } else {
-        if (es) k_qc_ms<C, false, true><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used);
-        else    k_qc_ms<C, false, false><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used);
+        const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
+#define FL(E, N) k_qc_ms<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used)
+#define FL2(N) do { if (es) FL(true, N); else FL(false, N); } while (0)
+        switch (norm) {
+            case NORM_PLAIN: FL2(NORM_PLAIN); break;
+            case NORM_ALPHA: FL2(NORM_ALPHA); break;
+            case NORM_BETA: FL2(NORM_BETA); break;
+            default: FL2(NORM_BOTH);
+        }
+#undef FL2
+#undef FL
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));

@@ -30,6 +30,9 @@ namespace ldpc {
 #ifndef QC_ID_AT_VN
 #define QC_ID_AT_VN 1  // find the min slot by |v| == min1 at VN time instead of tracking it in CN
 #endif
+#ifndef QC_DIAG_DPP
+#define QC_DIAG_DPP 0
+#endif
 #ifndef QC_ROW_BARRIER
 #define QC_ROW_BARRIER 0  // measured +1.9% without the per-row scheduling barrier
 #endif
@@ -107,7 +110,14 @@ __device__ __forceinline__ float mag_of(float m, float alpha, float beta, float 
 }
 
 __device__ __forceinline__ float bperm(int addr, float v) {
+#if QC_DIAG_DPP
+    // DIAGNOSTIC BUILD ONLY (wrong results): a VALU DPP move instead of the LDS-pipe permute, to price
+    // the ds_bpermute traffic.  The address stays live so its computation is still timed.
+    asm volatile("" ::"v"(addr));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, false));
+#else
     return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+#endif
 }
 
 // QUANT = false: float min-sum.  QUANT = true: integer offset min-sum carried in float registers (all
@@ -126,7 +136,12 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t cw = wave * CPW + half;
     const bool valid = (z < Z) && (cw < B);
-    const int base4 = lane * 4;
+    // Rotation bases.  Idle lanes (z >= Z) borrow the bases of lane z - Z of their group: their
+    // ds_bpermute sources then either coincide with an active lane's source (LDS broadcast) or fall on
+    // banks no active lane uses; with their own bases they caused ~1.7 bank-conflict cycles per
+    // bpermute (SQ_LDS_BANK_CONFLICT).
+    const int zb = (z < Z) ? z : z - Z;
+    const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
     // invalid lanes read element 0 (B >= 1) and discard it: unconditional loads, no per-load branches
     const float* lp = llr + (valid ? cw * N + z : 0);
@@ -176,8 +191,16 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
 #if QC_ROW_BARRIER
             __builtin_amdgcn_sched_barrier(0);
 #endif
+#if QC_ADDR_SGPR_MASK
+            // the volatile sel_lanes asm already keeps addresses per row; only the LDS base of the L
+            // reloads must be opaque (else LICM hoists the loop-invariant LDS loads: +24 VGPRs)
+            const int br = base4, bmr = base4m;
+            int lr = lbase;
+            asm volatile("" : "+v"(lr));
+#else
             int zr = z, br = base4, bmr = base4m, lr = lbase;
             asm volatile("" : "+v"(zr), "+v"(br), "+v"(bmr), "+v"(lr));
+#endif
             static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
                 constexpr int j = decltype(jj)::value;
                 if constexpr (first_row<C>(j) == r) nap[j] = Ls[lr + j * Z];

@@ -45,64 +45,136 @@ __global__ __launch_bounds__(256) void k_load_llr(const T* __restrict__ llr, T* 
     }
 }
 
+// V codewords per thread: every message access is a 16-byte-per-lane load/store (a wave moves 1 KiB per
+// instruction).  V = 4 floats (2 doubles) for small degrees; fewer when MAXD*V values would not fit.
+template <typename T, int MAXD>
+struct VW {
+    static constexpr int v16 = 16 / (int)sizeof(T);
+    static constexpr int value = (MAXD <= 8) ? v16 : (MAXD <= 16 ? (v16 >= 2 ? v16 / 2 : 1) : 1);
+};
+
+template <typename T, int V>
+struct Vec {
+    T x[V];
+};
+template <typename T, int V>
+__device__ __forceinline__ Vec<T, V> vload(const T* p) {
+    Vec<T, V> r;
+    if constexpr (V * sizeof(T) == 16) {
+        using U = __attribute__((ext_vector_type(4))) float;
+        const U u = *reinterpret_cast<const U*>(p);
+        __builtin_memcpy(r.x, &u, 16);
+    } else if constexpr (V * sizeof(T) == 8) {
+        using U = __attribute__((ext_vector_type(2))) float;
+        const U u = *reinterpret_cast<const U*>(p);
+        __builtin_memcpy(r.x, &u, 8);
+    } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) r.x[i] = p[i];
+    }
+    return r;
+}
+template <typename T, int V>
+__device__ __forceinline__ void vstore(T* p, const Vec<T, V>& r) {
+    if constexpr (V * sizeof(T) == 16) {
+        using U = __attribute__((ext_vector_type(4))) float;
+        U u;
+        __builtin_memcpy(&u, r.x, 16);
+        *reinterpret_cast<U*>(p) = u;
+    } else if constexpr (V * sizeof(T) == 8) {
+        using U = __attribute__((ext_vector_type(2))) float;
+        U u;
+        __builtin_memcpy(&u, r.x, 8);
+        *reinterpret_cast<U*>(p) = u;
+    } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) p[i] = r.x[i];
+    }
+}
+
+// Loads are issued for all MAXD slots with the edge index clamped to the last valid one (harmless
+// duplicate reads): a wave-uniform `if (k < d)` around each load makes hipcc branch around it and
+// drain vmcnt per load (cdna_hip_programming.md §5, load-reduce trap (c)).
+
 template <typename T, int MAXD>
 __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                const T* __restrict__ L, const T* __restrict__ c2v, T* __restrict__ v2c,
                                                int64_t B, int64_t ldb, int first) {
+    constexpr int V = VW<T, MAXD>::value;
     const int v = blockIdx.y;
-    const int64_t cw = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
     if (cw >= B) return;
     const int a = var_ptr[v];
     const int d = var_ptr[v + 1] - a;
-    const T Lv = L[(int64_t)v * ldb + cw];
-    T x[MAXD];
+    if (d == 0) return;  // an all-zero column of H has no messages (k_final still decides it)
+    const Vec<T, V> Lv = vload<T, V>(L + (int64_t)v * ldb + cw);
+    Vec<T, V> x[MAXD];
     int64_t off[MAXD];
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k)
-        if (k < d) {
-            off[k] = (int64_t)var_edges[a + k] * ldb + cw;
-            x[k] = first ? T(0) : c2v[off[k]];
+    for (int k = 0; k < MAXD; ++k) {
+        off[k] = (int64_t)var_edges[a + (k < d ? k : d - 1)] * ldb + cw;
+        if (first) {
+#pragma unroll
+            for (int i = 0; i < V; ++i) x[k].x[i] = T(0);
+        } else {
+            x[k] = vload<T, V>(c2v + off[k]);
         }
-    T P = T(0);
+    }
+    Vec<T, V> P;
+#pragma unroll
+    for (int i = 0; i < V; ++i) P.x[i] = T(0);
 #pragma unroll
     for (int t = 0; t < MAXD; ++t)
         if (t < d) {
-            T S = P;
+            Vec<T, V> o;
 #pragma unroll
-            for (int u = t + 1; u < MAXD; ++u)
-                if (u < d) S += x[u];
-            v2c[off[t]] = Num<T>::tanh_(T(0.5) * (Lv + S));
-            P += x[t];
+            for (int i = 0; i < V; ++i) {
+                T S = P.x[i];
+#pragma unroll
+                for (int u = t + 1; u < MAXD; ++u)
+                    if (u < d) S += x[u].x[i];
+                o.x[i] = Num<T>::tanh_(T(0.5) * (Lv.x[i] + S));
+                P.x[i] += x[t].x[i];
+            }
+            vstore<T, V>(v2c + off[t], o);
         }
 }
 
 template <typename T, int MAXD>
 __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_ptr, const T* __restrict__ v2c,
                                                T* __restrict__ c2v, int64_t B, int64_t ldb, T clamp) {
+    constexpr int V = VW<T, MAXD>::value;
     const int c = blockIdx.y;
-    const int64_t cw = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
     if (cw >= B) return;
     const int a = row_ptr[c];
     const int d = row_ptr[c + 1] - a;
-    T t[MAXD];
+    if (d == 0) return;  // an empty check carries no messages
+    Vec<T, V> t[MAXD];
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k)
-        if (k < d) t[k] = v2c[(int64_t)(a + k) * ldb + cw];
-    T Q = T(1);
+    for (int k = 0; k < MAXD; ++k) t[k] = vload<T, V>(v2c + (int64_t)(a + (k < d ? k : d - 1)) * ldb + cw);
+    Vec<T, V> Q;
+#pragma unroll
+    for (int i = 0; i < V; ++i) Q.x[i] = T(1);
 #pragma unroll
     for (int e = 0; e < MAXD; ++e)
         if (e < d) {
-            T p = Q;
+            Vec<T, V> o;
 #pragma unroll
-            for (int u = e + 1; u < MAXD; ++u)
-                if (u < d) p *= t[u];
-            if (p > Num<T>::pmax) p = Num<T>::pmax;
-            if (p < -Num<T>::pmax) p = -Num<T>::pmax;
-            T y = Num<T>::log_((T(1) + p) / (T(1) - p));
-            if (y > clamp) y = clamp;
-            if (y < -clamp) y = -clamp;
-            c2v[(int64_t)(a + e) * ldb + cw] = y;
-            Q *= t[e];
+            for (int i = 0; i < V; ++i) {
+                T p = Q.x[i];
+#pragma unroll
+                for (int u = e + 1; u < MAXD; ++u)
+                    if (u < d) p *= t[u].x[i];
+                if (p > Num<T>::pmax) p = Num<T>::pmax;
+                if (p < -Num<T>::pmax) p = -Num<T>::pmax;
+                T y = Num<T>::log_((T(1) + p) / (T(1) - p));
+                if (y > clamp) y = clamp;
+                if (y < -clamp) y = -clamp;
+                o.x[i] = y;
+                Q.x[i] *= t[e].x[i];
+            }
+            vstore<T, V>(c2v + (int64_t)(a + e) * ldb + cw, o);
         }
 }
 
@@ -110,61 +182,86 @@ template <int MAXD>
 __global__ __launch_bounds__(256) void k_vn_ms(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                const float* __restrict__ L, const float* __restrict__ c2v,
                                                float* __restrict__ v2c, int64_t B, int64_t ldb, int first) {
+    constexpr int V = VW<float, MAXD>::value;
     const int v = blockIdx.y;
-    const int64_t cw = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
     if (cw >= B) return;
     const int a = var_ptr[v];
     const int d = var_ptr[v + 1] - a;
-    float app = L[(int64_t)v * ldb + cw];
-    float x[MAXD];
+    if (d == 0) return;
+    Vec<float, V> app = vload<float, V>(L + (int64_t)v * ldb + cw);
+    Vec<float, V> x[MAXD];
     int64_t off[MAXD];
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+        off[k] = (int64_t)var_edges[a + (k < d ? k : d - 1)] * ldb + cw;
+        if (first) {
+#pragma unroll
+            for (int i = 0; i < V; ++i) x[k].x[i] = 0.0f;
+        } else {
+            x[k] = vload<float, V>(c2v + off[k]);
+        }
+    }
 #pragma unroll
     for (int k = 0; k < MAXD; ++k)
         if (k < d) {
-            off[k] = (int64_t)var_edges[a + k] * ldb + cw;
-            x[k] = first ? 0.0f : c2v[off[k]];
-            app += x[k];
+#pragma unroll
+            for (int i = 0; i < V; ++i) app.x[i] += x[k].x[i];
         }
 #pragma unroll
     for (int k = 0; k < MAXD; ++k)
-        if (k < d) v2c[off[k]] = app - x[k];
+        if (k < d) {
+            Vec<float, V> o;
+#pragma unroll
+            for (int i = 0; i < V; ++i) o.x[i] = app.x[i] - x[k].x[i];
+            vstore<float, V>(v2c + off[k], o);
+        }
 }
 
 template <int MAXD>
 __global__ __launch_bounds__(256) void k_cn_ms(const int32_t* __restrict__ row_ptr, const float* __restrict__ v2c,
                                                float* __restrict__ c2v, int64_t B, int64_t ldb, float clamp,
                                                float alpha, float beta) {
+    constexpr int V = VW<float, MAXD>::value;
     const int c = blockIdx.y;
-    const int64_t cw = (int64_t)blockIdx.x * kTB + threadIdx.x;
+    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
     if (cw >= B) return;
     const int a = row_ptr[c];
     const int d = row_ptr[c + 1] - a;
-    float t[MAXD];
-    float min1 = __builtin_inff(), min2 = __builtin_inff();
-    int idx = -1;
-    uint32_t sgn = 0;
+    if (d == 0) return;
+    Vec<float, V> t[MAXD];
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k)
-        if (k < d) {
-            t[k] = v2c[(int64_t)(a + k) * ldb + cw];
-            const float m = fabsf(t[k]);
-            sgn ^= f2u(t[k]);
-            if (m < min1) {
-                min2 = min1;
-                min1 = m;
-                idx = k;
-            } else if (m < min2) {
-                min2 = m;
+    for (int k = 0; k < MAXD; ++k) t[k] = vload<float, V>(v2c + (int64_t)(a + (k < d ? k : d - 1)) * ldb + cw);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        float min1 = __builtin_inff(), min2 = __builtin_inff();
+        int idx = -1;
+        uint32_t sgn = 0;
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k)
+            if (k < d) {
+                const float m = fabsf(t[k].x[i]);
+                sgn ^= f2u(t[k].x[i]);
+                if (m < min1) {
+                    min2 = min1;
+                    min1 = m;
+                    idx = k;
+                } else if (m < min2) {
+                    min2 = m;
+                }
             }
-        }
-    const float mag1 = ms_mag(min1, alpha, beta, clamp);
-    const float mag2 = ms_mag(min2, alpha, beta, clamp);
+        const float mag1 = ms_mag(min1, alpha, beta, clamp);
+        const float mag2 = ms_mag(min2, alpha, beta, clamp);
+#pragma unroll
+        for (int k = 0; k < MAXD; ++k)
+            if (k < d) {
+                const float mag = (k == idx) ? mag2 : mag1;
+                t[k].x[i] = u2f(f2u(mag) | ((sgn ^ f2u(t[k].x[i])) & 0x80000000u));
+            }
+    }
 #pragma unroll
     for (int k = 0; k < MAXD; ++k)
-        if (k < d) {
-            const float mag = (k == idx) ? mag2 : mag1;
-            c2v[(int64_t)(a + k) * ldb + cw] = u2f(f2u(mag) | ((sgn ^ f2u(t[k])) & 0x80000000u));
-        }
+        if (k < d) vstore<float, V>(c2v + (int64_t)(a + k) * ldb + cw, t[k]);
 }
 
 // Final VC + sigmoid + hard decision (bp/bp.py:36-39,51; ofdm_functions.py:161), transposed back to
@@ -211,7 +308,9 @@ __global__ __launch_bounds__(256) void k_final(const int32_t* __restrict__ var_p
 }
 
 // ------------------------------------------------------------------------------------------------
-static int pick_maxd(int d) { return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : d <= 32 ? 32 : -1; }
+static int pick_maxd(int d) {
+    return d <= 4 ? 4 : d <= 8 ? 8 : d <= 12 ? 12 : d <= 16 ? 16 : d <= 20 ? 20 : d <= 24 ? 24 : d <= 32 ? 32 : -1;
+}
 
 template <typename T>
 static int run_sp(const GenericArgs& g, const T* llr_dev, int64_t B, int iters, T clamp, uint8_t* bits, T* soft,
@@ -221,17 +320,17 @@ static int run_sp(const GenericArgs& g, const T* llr_dev, int64_t B, int iters, 
     T* v2c = L + (int64_t)g.n * ldb;
     T* c2v = v2c + (int64_t)g.E * ldb;
     const dim3 tb(kTB);
-    const unsigned gx = (unsigned)((B + kTB - 1) / kTB);
+    auto gxv = [B](int V) { return (unsigned)((B + (int64_t)kTB * V - 1) / ((int64_t)kTB * V)); };
     k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb);
     const int dv = pick_maxd(g.max_dv), dc = pick_maxd(g.max_dc);
     if (dv < 0 || dc < 0) return set_error(LDPC_EUNSUPPORTED, "node degree > 32 not supported by generic kernels");
     for (int it = 0; it < iters; ++it) {
         const int first = (it == 0);
-#define VN(D) k_vn_sp<T, D><<<dim3(gx, g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c, B, ldb, first)
-        switch (dv) { case 4: VN(4); break; case 8: VN(8); break; case 16: VN(16); break; default: VN(32); }
+#define VN(D) k_vn_sp<T, D><<<dim3(gxv(VW<T, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c, B, ldb, first)
+        switch (dv) { case 4: VN(4); break; case 8: VN(8); break; case 12: VN(12); break; case 16: VN(16); break; case 20: VN(20); break; case 24: VN(24); break; default: VN(32); }
 #undef VN
-#define CN(D) k_cn_sp<T, D><<<dim3(gx, g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp)
-        switch (dc) { case 4: CN(4); break; case 8: CN(8); break; case 16: CN(16); break; default: CN(32); }
+#define CN(D) k_cn_sp<T, D><<<dim3(gxv(VW<T, D>::value), g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp)
+        switch (dc) { case 4: CN(4); break; case 8: CN(8); break; case 12: CN(12); break; case 16: CN(16); break; case 20: CN(20); break; case 24: CN(24); break; default: CN(32); }
 #undef CN
     }
     if (iters == 0) (void)hipMemsetAsync(c2v, 0, sizeof(T) * (size_t)g.E * ldb, st);
@@ -247,17 +346,17 @@ static int run_ms(const GenericArgs& g, const float* llr_dev, int64_t B, int ite
     float* v2c = L + (int64_t)g.n * ldb;
     float* c2v = v2c + (int64_t)g.E * ldb;
     const dim3 tb(kTB);
-    const unsigned gx = (unsigned)((B + kTB - 1) / kTB);
+    auto gxv = [B](int V) { return (unsigned)((B + (int64_t)kTB * V - 1) / ((int64_t)kTB * V)); };
     k_load_llr<float><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb);
     const int dv = pick_maxd(g.max_dv), dc = pick_maxd(g.max_dc);
     if (dv < 0 || dc < 0) return set_error(LDPC_EUNSUPPORTED, "node degree > 32 not supported by generic kernels");
     for (int it = 0; it < iters; ++it) {
         const int first = (it == 0);
-#define VN(D) k_vn_ms<D><<<dim3(gx, g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c, B, ldb, first)
-        switch (dv) { case 4: VN(4); break; case 8: VN(8); break; case 16: VN(16); break; default: VN(32); }
+#define VN(D) k_vn_ms<D><<<dim3(gxv(VW<float, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c, B, ldb, first)
+        switch (dv) { case 4: VN(4); break; case 8: VN(8); break; case 12: VN(12); break; case 16: VN(16); break; case 20: VN(20); break; case 24: VN(24); break; default: VN(32); }
 #undef VN
-#define CN(D) k_cn_ms<D><<<dim3(gx, g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp, alpha, beta)
-        switch (dc) { case 4: CN(4); break; case 8: CN(8); break; case 16: CN(16); break; default: CN(32); }
+#define CN(D) k_cn_ms<D><<<dim3(gxv(VW<float, D>::value), g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp, alpha, beta)
+        switch (dc) { case 4: CN(4); break; case 8: CN(8); break; case 12: CN(12); break; case 16: CN(16); break; case 20: CN(20); break; case 24: CN(24); break; default: CN(32); }
 #undef CN
     }
     if (iters == 0) (void)hipMemsetAsync(c2v, 0, sizeof(float) * (size_t)g.E * ldb, st);

@@ -213,3 +213,16 @@ def test_qc_quantized_minsum_vs_oracle(code, early, beta):
     assert np.array_equal(r["iters_used"], ref["iters_used"])
     assert np.array_equal(r["bits"], ref["bits"])
     assert np.array_equal(r["soft"], (0.5 * ref["app"]).astype(np.float32))
+
+
+def test_degenerate_graph_empty_row_and_column():
+    """An all-zero row and column of H (the reference accepts any binary H, masking.py:12)."""
+    H, _ = get_code("peg64_32")
+    H = np.concatenate([H, np.zeros((1, 64), H.dtype)], axis=0)     # empty check
+    H = np.concatenate([H, np.zeros((33, 1), H.dtype)], axis=1)     # unconnected variable
+    rng = np.random.default_rng(4)
+    llr = rng.normal(2.0, 2.0, size=(100, 65)).astype(np.float32)
+    dec = ldpc_amd.get_decoder(H)
+    for algo, ref in (("minsum", oracle.ms_f32(H, llr, 7, 20.0)), ("tanh", oracle.sp_f32(H, llr, 7, 20.0))):
+        r = dec.decode(llr, 7, algo=algo, clamp=20.0, soft="z")
+        assert np.array_equal(r["bits"], ref["bits"])

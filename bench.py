@@ -55,8 +55,8 @@ def main():
     import torch.distributed as dist
     import ldpc_amd
     from ldpc_amd import _abi
-    from ldpc_amd.codes import Encoder
     from ldpc_amd.dist import allreduce_counts, max_over_ranks
+    from ldpc_amd.synth import DeviceEncoder
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -85,12 +85,10 @@ def main():
     st = stream.cuda_stream
 
     # ---- synthetic data, resident in HBM before timing -------------------------------------------
-    enc = Encoder(H)
-    gen = torch.Generator(device="cuda").manual_seed(args.seed + 7919 * rank)
-    info = torch.randint(0, 2, (B, k), generator=gen, device="cuda", dtype=torch.int32)
-    Gp = torch.from_numpy(enc.generator_parity().astype(np.float32)).cuda()
-    par = torch.remainder(info.float() @ Gp, 2.0).to(torch.uint8)
-    cw = torch.cat([info.to(torch.uint8), par], dim=1).contiguous()
+    enc = DeviceEncoder(H, torch.device("cuda", local))
+    info = torch.empty((B, k), dtype=torch.uint8, device="cuda")
+    _abi.check(lib.ldpc_random_bits(info.data_ptr(), B, k, args.seed, rank * B, st))
+    cw = enc.encode(info)
     llrs = []
     for i, e in enumerate(ebn0):
         sigma = float(np.sqrt(1.0 / (2.0 * rate * 10.0 ** (e / 10.0))))
@@ -141,7 +139,7 @@ def main():
     value = total_cw / elapsed
 
     # ---- roofline: algorithmic bytes per decode launch / event-timed launch duration ----
-    E = int(H.sum())
+    E = int(H.sum())  # nnz (SparseCode.sum() too)
     bpc = algorithmic_bytes_per_cw(n, E, args.iters)
     achieved = bpc * B / (gpu_ms * 1e-3) / 1e9
     peak = 8000.0
@@ -198,9 +196,9 @@ def cpu_baseline(H, args, rate):
     workload: same code, algorithm and iteration count, Eb/N0 = 2.5 dB.  CPU comparator only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    from ldpc_amd.codes import Encoder
+    from ldpc_amd.codes import Encoder, IRAEncoder, SparseCode
     rng = np.random.default_rng(5)
-    enc = Encoder(H)
+    enc = IRAEncoder(H) if isinstance(H, SparseCode) else Encoder(H)
 
     def sample(Bs):
         c = enc.encode(rng.integers(0, 2, size=(Bs, enc.k)))

@@ -22,7 +22,7 @@ import numpy as np
 
 from . import _abi
 from ._abi import Params, check
-from .codes import Graph
+from .codes import Graph, SparseCode
 
 _ALGOS = {"tanh": _abi.ALGO_TANH_SP, "sp": _abi.ALGO_TANH_SP, "tanh_sp": _abi.ALGO_TANH_SP,
           "minsum": _abi.ALGO_MIN_SUM, "min_sum": _abi.ALGO_MIN_SUM, "ms": _abi.ALGO_MIN_SUM,
@@ -39,8 +39,7 @@ class Decoder:
 
     def __init__(self, H, device: int = 0):
         self.lib = _abi.load()
-        H = np.asarray(H)
-        g = Graph.from_H(H)
+        g = Graph.from_H(H if isinstance(H, (SparseCode, Graph)) else np.asarray(H)) if not isinstance(H, Graph) else H
         self.m, self.n, self.E = g.m, g.n, g.E
         self.device = int(device)
         h = ctypes.c_void_p()
@@ -138,8 +137,11 @@ _cache_lock = threading.Lock()
 def get_decoder(H, device: int = 0) -> Decoder:
     """Graphs are built once per (H, device) — the reference rebuilt its dense masks on every
     decode_bits call (ofdm_functions.py:143/145)."""
-    H = np.asarray(H)
-    key = (H.shape, hashlib.sha1(np.packbits(H.astype(np.uint8) & 1).tobytes()).hexdigest(), int(device))
+    if isinstance(H, SparseCode):
+        key = (H.shape, hashlib.sha1(H.row_ptr.tobytes() + H.col_idx.tobytes()).hexdigest(), int(device))
+    else:
+        H = np.asarray(H)
+        key = (H.shape, hashlib.sha1(np.packbits(H.astype(np.uint8) & 1).tobytes()).hexdigest(), int(device))
     with _cache_lock:
         d = _cache.get(key)
         if d is None:
@@ -178,8 +180,9 @@ def decode_bits(llrs, H, bp_iterations, batch_size, clamp_value):
     rows = num_batches * batch_size
     if rows == 0:
         return output_bits
-    if llrs.ndim != 2 or llrs.shape[1] != np.asarray(H).shape[1]:
-        raise RuntimeError(f"llrs shape {llrs.shape} does not match H {np.asarray(H).shape}")
+    hshape = H.shape if isinstance(H, SparseCode) else np.asarray(H).shape
+    if llrs.ndim != 2 or llrs.shape[1] != hshape[1]:
+        raise RuntimeError(f"llrs shape {llrs.shape} does not match H {hshape}")
     dec = get_decoder(H)
     chunk = max(batch_size, (1 << 26) // max(dec.E, 1) // batch_size * batch_size)
     for s in range(0, rows, chunk):

@@ -144,13 +144,15 @@ def wifi_code(n: int, rate: str) -> QCCode:
 
 
 def available_codes():
-    return ["peg64_32"] + [f"wifi{n}_{r.replace('/', '')}" for (n, r) in sorted(_WIFI_TABLES)]
+    return ["peg64_32"] + [f"wifi{n}_{r.replace('/', '')}" for (n, r) in sorted(_WIFI_TABLES)] + ["dvbs2s_12"]
 
 
 def get_code(name: str):
     """Return ``(H, qc)`` for a named code; ``qc`` is the QCCode or ``None``."""
     if name == "peg64_32":
         return peg_64_32(), None
+    if name == "dvbs2s_12":
+        return dvbs2_shaped(), None
     if name.startswith("wifi"):
         body = name[4:]
         n, r = body.split("_")
@@ -184,7 +186,20 @@ class Graph:
         return int(self.col_idx.shape[0])
 
     @classmethod
+    def from_csr(cls, m: int, n: int, row_ptr, col_idx) -> "Graph":
+        row_ptr = np.asarray(row_ptr, np.int32)
+        col_idx = np.asarray(col_idx, np.int32)
+        rows = np.repeat(np.arange(m, dtype=np.int32), np.diff(row_ptr))
+        order = np.lexsort((rows, col_idx)).astype(np.int32)   # column-major = ascending check per column
+        var_ptr = np.zeros(n + 1, dtype=np.int32)
+        np.add.at(var_ptr, col_idx + 1, 1)
+        var_ptr = np.cumsum(var_ptr).astype(np.int32)
+        return cls(m, n, row_ptr, col_idx, var_ptr, order, rows)
+
+    @classmethod
     def from_H(cls, H) -> "Graph":
+        if isinstance(H, SparseCode):
+            return cls.from_csr(H.m, H.n, H.row_ptr, H.col_idx)
         H = np.asarray(H)
         if H.ndim != 2:
             raise ValueError("H must be a 2-D 0/1 matrix")
@@ -281,3 +296,104 @@ class Encoder:
     def generator_parity(self) -> np.ndarray:
         """(k, m) matrix Gp with parity = info @ Gp mod 2 (for device-side encoding)."""
         return self.P.T.copy()
+
+
+# ---------------------------------------------------------------------------------------------
+@dataclass
+class SparseCode:
+    """A parity-check matrix kept in CSR form only (codes too large for a dense H)."""
+
+    m: int
+    n: int
+    row_ptr: np.ndarray
+    col_idx: np.ndarray
+    name: str = ""
+    info_groups: np.ndarray = field(default=None, repr=False)   # IRA: [k // 360][deg] check addresses
+
+    @property
+    def shape(self):
+        return (self.m, self.n)
+
+    @property
+    def k(self) -> int:
+        return self.n - self.m
+
+    def sum(self) -> int:
+        return int(self.col_idx.shape[0])
+
+    def dense(self) -> np.ndarray:
+        H = np.zeros((self.m, self.n), np.int64)
+        for c in range(self.m):
+            H[c, self.col_idx[self.row_ptr[c]:self.row_ptr[c + 1]]] = 1
+        return H
+
+
+def dvbs2_shaped(seed: int = 2019) -> SparseCode:
+    """A DVB-S2-SHAPED normal-frame rate-1/2 IRA code: n = 64800, k = 32400, q = 90, 90 address rows
+    (36 of degree 8, 54 of degree 3), staircase accumulator parity — exactly the structure, degree
+    profile and edge count (E = 226,799) of EN 302 307 Table B.5, but with seeded pseudo-random
+    addresses: the standard's address table is not available offline.  Parity of the table contents is
+    therefore UNPINNED; the decoder does not care (it is the generic CSR path).
+
+    Info bit i of group g connects to checks (x + (i mod 360) * q) mod m for every address x of row g.
+    Each residue class mod q receives exactly 5 addresses, so every check has 5 info edges + 2 parity
+    edges (check 0: 1 parity edge), as in the standard."""
+    n, k, q, Z = 64800, 32400, 90, 360
+    m = n - k
+    rng = np.random.default_rng(seed)
+    degs = [8] * 36 + [3] * 54
+    # residues: each class 0..q-1 used exactly 5 times, distinct inside a row
+    while True:
+        pool = np.repeat(np.arange(q), 5)
+        rng.shuffle(pool)
+        rows, pos, ok = [], 0, True
+        for d in degs:
+            r = pool[pos:pos + d]
+            pos += d
+            if len(set(r.tolist())) != d:
+                ok = False
+                break
+            rows.append(r)
+        if ok:
+            break
+    groups = [r + q * rng.integers(0, Z, size=len(r)) for r in rows]
+    cols, chks = [], []
+    i = np.arange(Z)
+    for g, xs in enumerate(groups):
+        for x in xs:
+            chks.append((x + i * q) % m)
+            cols.append(g * Z + i)
+    # parity: check c touches parity bits c-1 (if c > 0) and c
+    c = np.arange(m)
+    chks += [c, c[1:]]
+    cols += [k + c, k + c[1:] - 1]
+    chks = np.concatenate(chks)
+    cols = np.concatenate(cols)
+    order = np.lexsort((cols, chks))
+    chks, cols = chks[order], cols[order]
+    row_ptr = np.zeros(m + 1, np.int64)
+    np.add.at(row_ptr, chks + 1, 1)
+    row_ptr = np.cumsum(row_ptr).astype(np.int32)
+    return SparseCode(m, n, row_ptr, cols.astype(np.int32), name="dvbs2s_12",
+                      info_groups=np.array([np.pad(g, (0, 8 - len(g)), constant_values=-1) for g in groups]))
+
+
+class IRAEncoder:
+    """Systematic encoder for a SparseCode with staircase parity (info first, then p_0..p_{m-1}):
+    p_c = p_{c-1} xor (sum of the info bits of check c)."""
+
+    def __init__(self, code: SparseCode):
+        self.code = code
+        self.m, self.n, self.k = code.m, code.n, code.k
+        rp, ci = code.row_ptr, code.col_idx
+        chk = np.repeat(np.arange(self.m), np.diff(rp))
+        info = ci < self.k
+        self._chk, self._col = chk[info], ci[info]
+
+    def encode(self, info_bits: np.ndarray) -> np.ndarray:
+        info_bits = np.atleast_2d(np.asarray(info_bits)).astype(np.uint8) & 1
+        B = info_bits.shape[0]
+        s = np.zeros((B, self.m), np.int64)
+        np.add.at(s.T, self._chk, info_bits[:, self._col].T)
+        par = np.cumsum(s, axis=1) & 1
+        return np.concatenate([info_bits, par.astype(np.uint8)], axis=1)

@@ -25,7 +25,8 @@ import numpy as np
 
 from . import _abi
 from .api import get_decoder
-from .codes import Encoder, get_code
+from .codes import get_code
+from .synth import DeviceEncoder
 from .dist import ebn0_sigma, sweep as dist_sweep
 
 
@@ -34,15 +35,14 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
         qmax=15, app_max=127):
     """Returns dict(snrdb, uncoded_ber, coded_ber, coded_bler, codewords, seconds)."""
     import torch
-    H, _ = get_code(code) if isinstance(code, str) else (np.asarray(code), None)
+    H, _ = get_code(code) if isinstance(code, str) else (code, None)
     m, n = H.shape
     k = n - m
     rate = k / n
     dec = get_decoder(H, device)
     lib = _abi.load()
-    enc = Encoder(H)
     dev = torch.device("cuda", device)
-    Gp = torch.from_numpy(enc.generator_parity().astype(np.float32)).to(dev)
+    enc = DeviceEncoder(H, dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     p = dec.params(iters, algo, clamp, alpha, beta, early_stop, "f32", "p1", qmax, app_max, qstep,
                    device_ptrs=True)
@@ -59,8 +59,7 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
         for s in range(lo, hi, bmax):
             B = min(bmax, hi - s)
             _abi.check(lib.ldpc_random_bits(info.data_ptr(), B, k, seed * 7919 + i, s, st))
-            par = torch.remainder(info[:B].float() @ Gp, 2.0).to(torch.uint8)
-            cw = torch.cat([info[:B], par], dim=1).contiguous()
+            cw = enc.encode(info[:B])
             _abi.check(lib.ldpc_awgn_llr(cw.data_ptr(), llr.data_ptr(), B, n, sigma, seed * 104729 + i, s, st))
             unc[i] += ((llr[:B] > 0).to(torch.uint8) != cw).sum()      # (np.sign(llr)+1)//2 decisions
             _abi.check(lib.ldpc_decode_ex(dec._h, llr.data_ptr(), B, p, bits.data_ptr(), None, None,

@@ -58,3 +58,17 @@ def test_qc_expand_shift_convention():
 def test_graph_rejects_non_binary():
     with pytest.raises(ValueError):
         Graph.from_H(np.array([[0, 2]]))
+
+
+def test_dvbs2_shaped_structure_and_encoder():
+    from ldpc_amd.codes import IRAEncoder, dvbs2_shaped
+    c = dvbs2_shaped()
+    g = Graph.from_H(c)
+    assert (c.m, c.n, g.E) == (32400, 64800, 226799)            # EN 302 307 normal frame, rate 1/2
+    dc = np.bincount(g.check_degrees())
+    assert dc[7] == 32399 and dc[6] == 1
+    dv = np.bincount(g.var_degrees())
+    assert dv[8] == 12960 and dv[3] == 19440 and dv[2] == 32399 and dv[1] == 1
+    cw = IRAEncoder(c).encode(np.random.default_rng(0).integers(0, 2, size=(2, c.k)))
+    for row in cw:
+        assert not (np.add.reduceat(row[c.col_idx].astype(np.int64), c.row_ptr[:-1]) % 2).any()

@@ -226,3 +226,19 @@ def test_degenerate_graph_empty_row_and_column():
     for algo, ref in (("minsum", oracle.ms_f32(H, llr, 7, 20.0)), ("tanh", oracle.sp_f32(H, llr, 7, 20.0))):
         r = dec.decode(llr, 7, algo=algo, clamp=20.0, soft="z")
         assert np.array_equal(r["bits"], ref["bits"])
+
+
+def test_dvbs2_shaped_minsum_bit_exact_and_sp_bits():
+    from ldpc_amd.codes import IRAEncoder, dvbs2_shaped
+    c = dvbs2_shaped()
+    rng = np.random.default_rng(9)
+    cw = IRAEncoder(c).encode(rng.integers(0, 2, size=(6, c.k)))
+    sigma = np.sqrt(1.0 / (2 * 0.5 * 10 ** (1.0 / 10)))
+    llr = (-2.0 * ((1.0 - 2.0 * cw) + sigma * rng.standard_normal(cw.shape)) / sigma**2).astype(np.float32)
+    dec = ldpc_amd.get_decoder(c)
+    r = dec.decode(torch.from_numpy(llr).cuda(), 12, algo="minsum", alpha=0.75, clamp=20.0, soft="z")
+    ref = oracle.ms_f32(c, llr, 12, 20.0, 0.75, 0.0)
+    assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])
+    assert np.array_equal(r["soft"].cpu().numpy().view(np.uint32), ref["z"].view(np.uint32))
+    r = dec.decode(llr, 6, algo="tanh", clamp=10.0)
+    assert (r["bits"] != oracle.sp_f32(c, llr, 6, 10.0)["bits"]).sum() == 0

@@ -17,7 +17,7 @@
 struct ldpc_graph {
     int m = 0, n = 0, E = 0, device = 0;
     int max_dc = 0, max_dv = 0;
-    int32_t *d_row_ptr = nullptr, *d_var_ptr = nullptr, *d_var_edges = nullptr;
+    int32_t *d_row_ptr = nullptr, *d_col_idx = nullptr, *d_var_ptr = nullptr, *d_var_edges = nullptr;
     const ldpc::QCSpec* qc = nullptr;
     std::mutex mtx;  // guards the internal workspace
     void* ws = nullptr;
@@ -145,6 +145,10 @@ static bool params_valid(const ldpc_params* p) {
     return true;
 }
 
+static GenericArgs gargs(const ldpc_graph* g) {
+    return GenericArgs{g->d_row_ptr, g->d_col_idx, g->d_var_ptr, g->d_var_edges, g->m, g->n, g->E, g->max_dc, g->max_dv};
+}
+
 static bool use_qc(const ldpc_graph* g, const ldpc_params* p) {
     return g->qc && !(p->flags & LDPC_F_FORCE_GENERIC) && qc_supports(g->qc, *p);
 }
@@ -154,7 +158,7 @@ static size_t elem_size(const ldpc_params* p) { return (p->flags & LDPC_F_F64) ?
 // Workspace = kernel scratch followed (host-pointer callers only) by staging for llr/bits/soft/used.
 static size_t kernel_ws(const ldpc_graph* g, int64_t B, const ldpc_params* p) {
     if (use_qc(g, p)) return align256(qc_workspace(g->qc, B, *p));
-    return align256(generic_workspace(g->n, g->E, B, elem_size(p)));
+    return align256(generic_workspace(gargs(g), B, *p));
 }
 static size_t staging_ws(const ldpc_graph* g, int64_t B, const ldpc_params* p) {
     if (p->flags & LDPC_F_DEVICE_PTRS) return 0;
@@ -186,7 +190,8 @@ static int build_graph(ldpc_graph* g, int m, int n, const std::vector<int32_t>& 
         return hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice);
     };
     hipError_t e;
-    if ((e = up(&g->d_row_ptr, row_ptr)) != hipSuccess || (e = up(&g->d_var_ptr, var_ptr)) != hipSuccess ||
+    if ((e = up(&g->d_row_ptr, row_ptr)) != hipSuccess || (e = up(&g->d_col_idx, col_idx)) != hipSuccess ||
+        (e = up(&g->d_var_ptr, var_ptr)) != hipSuccess ||
         (e = up(&g->d_var_edges, var_edges)) != hipSuccess)
         return set_error(e == hipErrorOutOfMemory ? LDPC_ENOMEM : LDPC_EHIP, "graph upload: %s", hipGetErrorString(e));
     return LDPC_OK;
@@ -288,6 +293,7 @@ int ldpc_graph_destroy(ldpc_graph* g) {
     if (!g) return LDPC_OK;
     DeviceGuard dg(g->device);
     (void)hipFree(g->d_row_ptr);
+    (void)hipFree(g->d_col_idx);
     (void)hipFree(g->d_var_ptr);
     (void)hipFree(g->d_var_edges);
     if (g->ws) (void)hipFree(g->ws);
@@ -363,8 +369,7 @@ int ldpc_decode_ex(const ldpc_graph* gc, const void* llr, int64_t B, const ldpc_
     if (use_qc(g, p)) {
         rc = qc_decode(g->qc, llr_d, B, *p, bits_d, soft_d, used_d, ws, st);
     } else {
-        GenericArgs ga{g->d_row_ptr, g->d_var_ptr, g->d_var_edges, g->m, g->n, g->E, g->max_dc, g->max_dv};
-        rc = generic_decode(ga, llr_d, B, *p, bits_d, soft_d, used_d, ws, st);
+        rc = generic_decode(gargs(g), llr_d, B, *p, bits_d, soft_d, used_d, ws, st);
     }
     if (rc != LDPC_OK) return rc;
     if (!dev) {

@@ -71,10 +71,10 @@ int set_error(int code, const char* fmt, ...);
 int fill_i32(int32_t* p, int64_t count, int32_t value, hipStream_t st);
 
 struct GenericArgs {
-    const int32_t *row_ptr, *var_ptr, *var_edges;
+    const int32_t *row_ptr, *col_idx, *var_ptr, *var_edges;
     int m, n, E, max_dc, max_dv;
 };
-size_t generic_workspace(int n, int E, int64_t B, size_t elem);
+size_t generic_workspace(const GenericArgs& g, int64_t B, const ldpc_params& p);
 int generic_decode(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,
                    void* soft, int32_t* iters_used, char* ws, hipStream_t st);
 

@@ -92,18 +92,83 @@ __device__ __forceinline__ void vstore(T* p, const Vec<T, V>& r) {
     }
 }
 
+// Early stop: codewords whose syndrome was zero are frozen (their c2v is never written again).
+template <int V>
+__device__ __forceinline__ bool all_done(const uint8_t* done) {
+    bool a = true;
+#pragma unroll
+    for (int i = 0; i < V; ++i) a = a && done[i];
+    return a;
+}
+template <typename T, int V, bool ES>
+__device__ __forceinline__ void store_live(T* p, const Vec<T, V>& r, const uint8_t* done) {
+    if constexpr (!ES) {
+        vstore<T, V>(p, r);
+    } else {
+        bool any = false;
+#pragma unroll
+        for (int i = 0; i < V; ++i) any = any || done[i];
+        if (!any) {
+            vstore<T, V>(p, r);
+        } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i)
+                if (!done[i]) p[i] = r.x[i];
+        }
+    }
+}
+
+// Syndrome of the hard decisions hb[n][ldb] (written by the VN kernel from APP_it): one thread per
+// (check, 4 codewords); any odd check marks its codeword unsatisfied (all writers store 1: benign).
+__global__ __launch_bounds__(256) void k_syndrome(const int32_t* __restrict__ row_ptr, const int32_t* __restrict__ col_idx,
+                                                  const uint8_t* __restrict__ hb, const uint8_t* __restrict__ done,
+                                                  uint8_t* __restrict__ unsat, int64_t B, int64_t ldb) {
+    const int c = blockIdx.y;
+    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * 4;
+    if (cw >= B) return;
+    const uint32_t dn = *reinterpret_cast<const uint32_t*>(done + cw);
+    if (dn == 0x01010101u) return;
+    uint32_t par = 0;
+    for (int e = row_ptr[c]; e < row_ptr[c + 1]; ++e)
+        par ^= *reinterpret_cast<const uint32_t*>(hb + (int64_t)col_idx[e] * ldb + cw);
+    par &= 0x01010101u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if ((par >> (8 * i)) & 1u) unsat[cw + i] = 1;
+}
+
+// After the syndrome of APP_it (it >= 1): converged codewords become done with iters_used = it.
+__global__ __launch_bounds__(256) void k_converge(uint8_t* __restrict__ done, uint8_t* __restrict__ unsat,
+                                                  int32_t* __restrict__ used, int64_t B, int it) {
+    const int64_t cw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cw >= B) return;
+    if (!done[cw] && !unsat[cw]) {
+        done[cw] = 1;
+        used[cw] = it;
+    }
+    unsat[cw] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_used_final(const uint8_t* __restrict__ done, int32_t* __restrict__ used,
+                                                    int64_t B, int iters) {
+    const int64_t cw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cw < B && !done[cw]) used[cw] = iters;
+}
+
 // Loads are issued for all MAXD slots with the edge index clamped to the last valid one (harmless
 // duplicate reads): a wave-uniform `if (k < d)` around each load makes hipcc branch around it and
 // drain vmcnt per load (cdna_hip_programming.md §5, load-reduce trap (c)).
 
-template <typename T, int MAXD>
+template <typename T, int MAXD, bool ES>
 __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                const T* __restrict__ L, const T* __restrict__ c2v, T* __restrict__ v2c,
-                                               int64_t B, int64_t ldb, int first) {
+                                               int64_t B, int64_t ldb, int first, uint8_t* __restrict__ hb,
+                                               const uint8_t* __restrict__ done) {
     constexpr int V = VW<T, MAXD>::value;
     const int v = blockIdx.y;
     const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
     if (cw >= B) return;
+    if (ES && all_done<V>(done + cw)) return;
     const int a = var_ptr[v];
     const int d = var_ptr[v + 1] - a;
     if (d == 0) return;  // an all-zero column of H has no messages (k_final still decides it)
@@ -138,15 +203,21 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
             }
             vstore<T, V>(v2c + off[t], o);
         }
+    if constexpr (ES) {  // hard decision of APP_it = the final layer's z (bp.py:36-39,51)
+#pragma unroll
+        for (int i = 0; i < V; ++i) hb[(int64_t)v * ldb + cw + i] = (uint8_t)Num<T>::bit(T(0.5) * (Lv.x[i] + P.x[i]));
+    }
 }
 
-template <typename T, int MAXD>
+template <typename T, int MAXD, bool ES>
 __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_ptr, const T* __restrict__ v2c,
-                                               T* __restrict__ c2v, int64_t B, int64_t ldb, T clamp) {
+                                               T* __restrict__ c2v, int64_t B, int64_t ldb, T clamp,
+                                               const uint8_t* __restrict__ done) {
     constexpr int V = VW<T, MAXD>::value;
     const int c = blockIdx.y;
     const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
     if (cw >= B) return;
+    if (ES && all_done<V>(done + cw)) return;
     const int a = row_ptr[c];
     const int d = row_ptr[c + 1] - a;
     if (d == 0) return;  // an empty check carries no messages
@@ -174,18 +245,20 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
                 o.x[i] = y;
                 Q.x[i] *= t[e].x[i];
             }
-            vstore<T, V>(c2v + (int64_t)(a + e) * ldb + cw, o);
+            store_live<T, V, ES>(c2v + (int64_t)(a + e) * ldb + cw, o, done + cw);
         }
 }
 
-template <int MAXD>
+template <int MAXD, bool ES>
 __global__ __launch_bounds__(256) void k_vn_ms(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                const float* __restrict__ L, const float* __restrict__ c2v,
-                                               float* __restrict__ v2c, int64_t B, int64_t ldb, int first) {
+                                               float* __restrict__ v2c, int64_t B, int64_t ldb, int first,
+                                               uint8_t* __restrict__ hb, const uint8_t* __restrict__ done) {
     constexpr int V = VW<float, MAXD>::value;
     const int v = blockIdx.y;
     const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
     if (cw >= B) return;
+    if (ES && all_done<V>(done + cw)) return;
     const int a = var_ptr[v];
     const int d = var_ptr[v + 1] - a;
     if (d == 0) return;
@@ -216,16 +289,21 @@ __global__ __launch_bounds__(256) void k_vn_ms(const int32_t* __restrict__ var_p
             for (int i = 0; i < V; ++i) o.x[i] = app.x[i] - x[k].x[i];
             vstore<float, V>(v2c + off[k], o);
         }
+    if constexpr (ES) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) hb[(int64_t)v * ldb + cw + i] = (uint8_t)(0.5f * app.x[i] <= kZthrF32);
+    }
 }
 
-template <int MAXD>
+template <int MAXD, bool ES>
 __global__ __launch_bounds__(256) void k_cn_ms(const int32_t* __restrict__ row_ptr, const float* __restrict__ v2c,
                                                float* __restrict__ c2v, int64_t B, int64_t ldb, float clamp,
-                                               float alpha, float beta) {
+                                               float alpha, float beta, const uint8_t* __restrict__ done) {
     constexpr int V = VW<float, MAXD>::value;
     const int c = blockIdx.y;
     const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
     if (cw >= B) return;
+    if (ES && all_done<V>(done + cw)) return;
     const int a = row_ptr[c];
     const int d = row_ptr[c + 1] - a;
     if (d == 0) return;
@@ -261,7 +339,7 @@ __global__ __launch_bounds__(256) void k_cn_ms(const int32_t* __restrict__ row_p
     }
 #pragma unroll
     for (int k = 0; k < MAXD; ++k)
-        if (k < d) vstore<float, V>(c2v + (int64_t)(a + k) * ldb + cw, t[k]);
+        if (k < d) store_live<float, V, ES>(c2v + (int64_t)(a + k) * ldb + cw, t[k], done + cw);
 }
 
 // Final VC + sigmoid + hard decision (bp/bp.py:36-39,51; ofdm_functions.py:161), transposed back to
@@ -312,86 +390,131 @@ static int pick_maxd(int d) {
     return d <= 4 ? 4 : d <= 8 ? 8 : d <= 12 ? 12 : d <= 16 ? 16 : d <= 20 ? 20 : d <= 24 ? 24 : d <= 32 ? 32 : -1;
 }
 
-template <typename T>
-static int run_sp(const GenericArgs& g, const T* llr_dev, int64_t B, int iters, T clamp, uint8_t* bits, T* soft,
-                  int soft_z, char* ws, hipStream_t st) {
+static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Workspace: L[n][ldb], v2c[E][ldb], c2v[E][ldb] (elem bytes each) and, with early stop,
+// hb[n][ldb] (uint8 hard decisions), done[ldb], unsat[ldb], used[ldb] (int32 scratch).
+struct WsLayout {
+    size_t L, v2c, c2v, hb, done, unsat, used, total;
+};
+static WsLayout layout(const GenericArgs& g, int64_t B, size_t elem, bool es) {
     const int64_t ldb = (B + 63) / 64 * 64;
-    T* L = (T*)ws;
-    T* v2c = L + (int64_t)g.n * ldb;
-    T* c2v = v2c + (int64_t)g.E * ldb;
+    WsLayout w{};
+    size_t off = 0;
+    w.L = off;
+    off += a256(elem * (size_t)ldb * g.n);
+    w.v2c = off;
+    off += a256(elem * (size_t)ldb * g.E);
+    w.c2v = off;
+    off += a256(elem * (size_t)ldb * g.E);
+    if (es) {
+        w.hb = off;
+        off += a256((size_t)ldb * g.n);
+        w.done = off;
+        off += a256((size_t)ldb);
+        w.unsat = off;
+        off += a256((size_t)ldb);
+        w.used = off;
+        off += a256((size_t)ldb * 4);
+    }
+    w.total = off;
+    return w;
+}
+
+size_t generic_workspace(const GenericArgs& g, int64_t B, const ldpc_params& p) {
+    const size_t elem = (p.flags & LDPC_F_F64) ? 8 : 4;
+    return layout(g, B, elem, (p.flags & LDPC_F_EARLY_STOP) != 0).total;
+}
+
+// One driver for both algorithms: VN and CN kernels per iteration (plus, with early stop, the
+// syndrome of APP_it and the convergence update between them), then the final decision kernel.
+template <typename T, bool MS, bool ES>
+static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits, T* soft,
+               int32_t* iters_used, char* ws, hipStream_t st) {
+    const int64_t ldb = (B + 63) / 64 * 64;
+    const WsLayout w = layout(g, B, sizeof(T), ES);
+    T* L = (T*)(ws + w.L);
+    T* v2c = (T*)(ws + w.v2c);
+    T* c2v = (T*)(ws + w.c2v);
+    uint8_t* hb = ES ? (uint8_t*)(ws + w.hb) : nullptr;
+    uint8_t* done = ES ? (uint8_t*)(ws + w.done) : nullptr;
+    uint8_t* unsat = ES ? (uint8_t*)(ws + w.unsat) : nullptr;
+    int32_t* used = ES ? (iters_used ? iters_used : (int32_t*)(ws + w.used)) : nullptr;
+    const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
+    const T clamp = (T)p.clamp;
     const dim3 tb(kTB);
     auto gxv = [B](int V) { return (unsigned)((B + (int64_t)kTB * V - 1) / ((int64_t)kTB * V)); };
+    const unsigned gcw = (unsigned)((B + kTB - 1) / kTB);
     k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb);
+    if (ES) {
+        if (hipMemsetAsync(done, 0, (size_t)ldb, st) != hipSuccess || hipMemsetAsync(unsat, 0, (size_t)ldb, st) != hipSuccess)
+            return set_error(LDPC_EHIP, "early-stop state init failed");
+    }
     const int dv = pick_maxd(g.max_dv), dc = pick_maxd(g.max_dc);
     if (dv < 0 || dc < 0) return set_error(LDPC_EUNSUPPORTED, "node degree > 32 not supported by generic kernels");
-    for (int it = 0; it < iters; ++it) {
+    for (int it = 0; it < p.iters; ++it) {
         const int first = (it == 0);
-#define VN(D) k_vn_sp<T, D><<<dim3(gxv(VW<T, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c, B, ldb, first)
+#define VN(D)                                                                                                      \
+    do {                                                                                                           \
+        if constexpr (MS)                                                                                          \
+            k_vn_ms<D, ES><<<dim3(gxv(VW<float, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, (const float*)L, \
+                (const float*)c2v, (float*)v2c, B, ldb, first, hb, done);                                         \
+        else                                                                                                       \
+            k_vn_sp<T, D, ES><<<dim3(gxv(VW<T, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c,   \
+                B, ldb, first, hb, done);                                                                          \
+    } while (0)
         switch (dv) { case 4: VN(4); break; case 8: VN(8); break; case 12: VN(12); break; case 16: VN(16); break; case 20: VN(20); break; case 24: VN(24); break; default: VN(32); }
 #undef VN
-#define CN(D) k_cn_sp<T, D><<<dim3(gxv(VW<T, D>::value), g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp)
+        if (ES && it > 0) {  // the oracle tests the syndrome of APP after each iteration >= 1
+            k_syndrome<<<dim3((unsigned)((B + 4 * kTB - 1) / (4 * kTB)), g.m), tb, 0, st>>>(g.row_ptr, g.col_idx, hb,
+                                                                                          done, unsat, B, ldb);
+            k_converge<<<gcw, tb, 0, st>>>(done, unsat, used, B, it);
+        }
+#define CN(D)                                                                                                      \
+    do {                                                                                                           \
+        if constexpr (MS)                                                                                          \
+            k_cn_ms<D, ES><<<dim3(gxv(VW<float, D>::value), g.m), tb, 0, st>>>(g.row_ptr, (const float*)v2c,        \
+                (float*)c2v, B, ldb, p.clamp, p.alpha, p.beta, done);                                              \
+        else                                                                                                       \
+            k_cn_sp<T, D, ES><<<dim3(gxv(VW<T, D>::value), g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp, done); \
+    } while (0)
         switch (dc) { case 4: CN(4); break; case 8: CN(8); break; case 12: CN(12); break; case 16: CN(16); break; case 20: CN(20); break; case 24: CN(24); break; default: CN(32); }
 #undef CN
     }
-    if (iters == 0) (void)hipMemsetAsync(c2v, 0, sizeof(T) * (size_t)g.E * ldb, st);
-    k_final<T, 32, false><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(
-        g.var_ptr, g.var_edges, L, c2v, B, ldb, g.n, bits, soft, soft_z);
-    return LDPC_OK;
-}
-
-static int run_ms(const GenericArgs& g, const float* llr_dev, int64_t B, int iters, float clamp, float alpha, float beta,
-                  uint8_t* bits, float* soft, int soft_z, char* ws, hipStream_t st) {
-    const int64_t ldb = (B + 63) / 64 * 64;
-    float* L = (float*)ws;
-    float* v2c = L + (int64_t)g.n * ldb;
-    float* c2v = v2c + (int64_t)g.E * ldb;
-    const dim3 tb(kTB);
-    auto gxv = [B](int V) { return (unsigned)((B + (int64_t)kTB * V - 1) / ((int64_t)kTB * V)); };
-    k_load_llr<float><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb);
-    const int dv = pick_maxd(g.max_dv), dc = pick_maxd(g.max_dc);
-    if (dv < 0 || dc < 0) return set_error(LDPC_EUNSUPPORTED, "node degree > 32 not supported by generic kernels");
-    for (int it = 0; it < iters; ++it) {
-        const int first = (it == 0);
-#define VN(D) k_vn_ms<D><<<dim3(gxv(VW<float, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c, B, ldb, first)
-        switch (dv) { case 4: VN(4); break; case 8: VN(8); break; case 12: VN(12); break; case 16: VN(16); break; case 20: VN(20); break; case 24: VN(24); break; default: VN(32); }
-#undef VN
-#define CN(D) k_cn_ms<D><<<dim3(gxv(VW<float, D>::value), g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp, alpha, beta)
-        switch (dc) { case 4: CN(4); break; case 8: CN(8); break; case 12: CN(12); break; case 16: CN(16); break; case 20: CN(20); break; case 24: CN(24); break; default: CN(32); }
-#undef CN
+    if (p.iters == 0) (void)hipMemsetAsync(c2v, 0, sizeof(T) * (size_t)g.E * ldb, st);
+    k_final<T, 32, MS><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, B,
+                                                                                      ldb, g.n, bits, soft, soft_z);
+    if (ES) {
+        k_used_final<<<gcw, tb, 0, st>>>(done, used, B, p.iters);
+    } else if (iters_used) {
+        fill_i32(iters_used, B, p.iters, st);  // every codeword runs the fixed iteration count
     }
-    if (iters == 0) (void)hipMemsetAsync(c2v, 0, sizeof(float) * (size_t)g.E * ldb, st);
-    k_final<float, 32, true><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(
-        g.var_ptr, g.var_edges, L, c2v, B, ldb, g.n, bits, soft, soft_z);
     return LDPC_OK;
-}
-
-size_t generic_workspace(int n, int E, int64_t B, size_t elem) {
-    const int64_t ldb = (B + 63) / 64 * 64;
-    return elem * (size_t)ldb * ((size_t)n + 2 * (size_t)E);
 }
 
 int generic_decode(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,
                    void* soft, int32_t* iters_used, char* ws, hipStream_t st) {
-    const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
-    if (p.flags & LDPC_F_EARLY_STOP)
-        return set_error(LDPC_EUNSUPPORTED, "early stop is implemented by the QC kernels only");
+    const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
     int rc;
     if (p.algo == LDPC_ALGO_TANH_SP) {
-        if (p.flags & LDPC_F_F64)
-            rc = run_sp<double>(g, (const double*)llr_dev, B, p.iters, (double)p.clamp, bits, (double*)soft, soft_z, ws, st);
-        else
-            rc = run_sp<float>(g, (const float*)llr_dev, B, p.iters, p.clamp, bits, (float*)soft, soft_z, ws, st);
+        if (p.flags & LDPC_F_F64) {
+            const double* x = (const double*)llr_dev;
+            rc = es ? run<double, false, true>(g, x, B, p, bits, (double*)soft, iters_used, ws, st)
+                    : run<double, false, false>(g, x, B, p, bits, (double*)soft, iters_used, ws, st);
+        } else {
+            const float* x = (const float*)llr_dev;
+            rc = es ? run<float, false, true>(g, x, B, p, bits, (float*)soft, iters_used, ws, st)
+                    : run<float, false, false>(g, x, B, p, bits, (float*)soft, iters_used, ws, st);
+        }
     } else if (p.algo == LDPC_ALGO_MIN_SUM) {
         if (p.flags & LDPC_F_F64) return set_error(LDPC_EUNSUPPORTED, "min-sum is float32 only");
-        rc = run_ms(g, (const float*)llr_dev, B, p.iters, p.clamp, p.alpha, p.beta, bits, (float*)soft, soft_z, ws, st);
+        const float* x = (const float*)llr_dev;
+        rc = es ? run<float, true, true>(g, x, B, p, bits, (float*)soft, iters_used, ws, st)
+                : run<float, true, false>(g, x, B, p, bits, (float*)soft, iters_used, ws, st);
     } else {
         return set_error(LDPC_EUNSUPPORTED, "algo %d not supported by the generic kernels", p.algo);
     }
     if (rc != LDPC_OK) return rc;
-    if (iters_used) {
-        // every codeword runs the fixed iteration count
-        rc = fill_i32(iters_used, B, p.iters, st);
-    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "generic kernel launch: %s", hipGetErrorString(e));
     return rc;

@@ -52,11 +52,25 @@ typedef struct {
 
 /* ------------------------------------------------------------------------------------------ */
 /* tanh sum-product, fp32 (bp/bp.py:43-51, bp_vc.py:16-27, bp_cv.py:22-50)                      */
-static void sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp, float* x, float* v2c,
-                       float* p1_out, float* z_out, uint8_t* bits_out, float* trace, int64_t trace_stride) {
+static int syndrome_ok(const graph_t* g, const uint8_t* bits);
+
+/* early stop (not in the reference): after iteration it >= 1, stop when the final layer's decisions
+ * z = 0.5*(L + sum x) (bp.py:36-39,51) satisfy every check; returns the iterations run. */
+static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp, float* x, float* v2c,
+                      float* p1_out, float* z_out, uint8_t* bits_out, float* trace, int64_t trace_stride,
+                      int early_stop, uint8_t* hb) {
     const int E = g->E;
+    int used = iters;
     for (int e = 0; e < E; ++e) x[e] = 0.0f;
     for (int it = 0; it < iters; ++it) {
+        if (early_stop && it > 0) {
+            for (int v = 0; v < g->n; ++v) {
+                float S = 0.0f;
+                for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += x[g->var_edges[u]];
+                hb[v] = (uint8_t)(0.5f * (-llr[v] + S) <= ZTHR_F32);
+            }
+            if (syndrome_ok(g, hb)) { used = it; break; }
+        }
         /* VC + tanh: v2c at check-order ids */
         for (int v = 0; v < g->n; ++v) {
             const int a = g->var_ptr[v], b = g->var_ptr[v + 1];
@@ -93,6 +107,7 @@ static void sp_f32_one(const graph_t* g, const float* llr, int iters, float clam
         if (p1_out) p1_out[v] = 1.0f - 1.0f / (1.0f + expf(-z));
         if (bits_out) bits_out[v] = (uint8_t)(z <= ZTHR_F32);
     }
+    return used;
 }
 
 /* tanh sum-product, fp64: the reference module after .double() */
@@ -259,18 +274,22 @@ static int qms_one(const graph_t* g, const int8_t* qllr, int iters, int qmax, in
 #define MAKE_GRAPH graph_t g = {m, n, E, row_ptr, col_idx, var_ptr, var_edges}
 
 int oracle_sp_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clamp, float* p1, float* z,
-                  uint8_t* bits, float* trace /* [iters][B][E] or NULL */) {
+                  uint8_t* bits, float* trace /* [iters][B][E] or NULL */, int early_stop, int32_t* iters_used) {
     MAKE_GRAPH;
 #pragma omp parallel
     {
         float* x = (float*)malloc(sizeof(float) * (size_t)E);
         float* v2c = (float*)malloc(sizeof(float) * (size_t)E);
+        uint8_t* hb = (uint8_t*)malloc((size_t)n);
 #pragma omp for schedule(dynamic, 16)
-        for (int64_t i = 0; i < B; ++i)
-            sp_f32_one(&g, llr + i * n, iters, clamp, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
-                       bits ? bits + i * n : NULL, trace ? trace + i * E : NULL, B * (int64_t)E);
+        for (int64_t i = 0; i < B; ++i) {
+            int u = sp_f32_one(&g, llr + i * n, iters, clamp, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
+                               bits ? bits + i * n : NULL, trace ? trace + i * E : NULL, B * (int64_t)E, early_stop, hb);
+            if (iters_used) iters_used[i] = u;
+        }
         free(x);
         free(v2c);
+        free(hb);
     }
     return 0;
 }

@@ -36,7 +36,8 @@ def lib():
         i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
         vp = ctypes.c_void_p
         garg = [ctypes.c_int, ctypes.c_int, ctypes.c_int, i32p, i32p, i32p, i32p]
-        L.oracle_sp_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, vp, vp, vp, vp]
+        L.oracle_sp_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, vp, vp, vp, vp,
+                                           ctypes.c_int, vp]
         L.oracle_sp_f64.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, vp, vp, vp]
         L.oracle_ms_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                            ctypes.c_float, ctypes.c_int, vp, vp, vp, vp]
@@ -61,8 +62,8 @@ def _gargs(g: Graph):
     return (g.m, g.n, g.E, g.row_ptr, g.col_idx, g.var_ptr, g.var_edges)
 
 
-def sp_f32(H, llr, iters, clamp, trace=False):
-    """tanh sum-product in fp32. Returns dict(p1, z, bits[, trace[iters,B,E]])."""
+def sp_f32(H, llr, iters, clamp, trace=False, early_stop=False):
+    """tanh sum-product in fp32. Returns dict(p1, z, bits, iters_used[, trace[iters,B,E]])."""
     g = _graph(H)
     llr = np.ascontiguousarray(llr, dtype=np.float32)
     B = llr.shape[0]
@@ -70,8 +71,10 @@ def sp_f32(H, llr, iters, clamp, trace=False):
     z = np.empty((B, g.n), np.float32)
     bits = np.empty((B, g.n), np.uint8)
     tr = np.empty((iters, B, g.E), np.float32) if trace else None
-    lib().oracle_sp_f32(*_gargs(g), _ptr(llr), B, int(iters), float(clamp), _ptr(p1), _ptr(z), _ptr(bits), _ptr(tr))
-    out = dict(p1=p1, z=z, bits=bits)
+    used = np.empty(B, np.int32)
+    lib().oracle_sp_f32(*_gargs(g), _ptr(llr), B, int(iters), float(clamp), _ptr(p1), _ptr(z), _ptr(bits), _ptr(tr),
+                        int(bool(early_stop)), _ptr(used))
+    out = dict(p1=p1, z=z, bits=bits, iters_used=used)
     if trace:
         out["trace"] = tr
     return out

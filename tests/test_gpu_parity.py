@@ -242,3 +242,21 @@ def test_dvbs2_shaped_minsum_bit_exact_and_sp_bits():
     assert np.array_equal(r["soft"].cpu().numpy().view(np.uint32), ref["z"].view(np.uint32))
     r = dec.decode(llr, 6, algo="tanh", clamp=10.0)
     assert (r["bits"] != oracle.sp_f32(c, llr, 6, 10.0)["bits"]).sum() == 0
+
+
+@pytest.mark.parametrize("code", ["peg64_32", "wifi648_12", "wifi1944_56"])
+@pytest.mark.parametrize("algo", ["minsum", "tanh"])
+def test_generic_early_stop_vs_oracle(code, algo):
+    H, _ = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, 301, 2.5 if rate < 0.6 else 4.5, seed=31, rate=rate)
+    dec = ldpc_amd.get_decoder(H)
+    r = dec.decode(llr, 20, algo=algo, clamp=20.0, early_stop=True, force_generic=True, want_iters=True, soft="z")
+    if algo == "minsum":
+        ref = oracle.ms_f32(H, llr, 20, 20.0, early_stop=True)
+        assert np.array_equal(r["soft"].view(np.uint32), ref["z"].view(np.uint32))
+    else:
+        ref = oracle.sp_f32(H, llr, 20, 20.0, early_stop=True)
+    assert np.array_equal(r["iters_used"], ref["iters_used"])
+    assert np.array_equal(r["bits"], ref["bits"])
+    assert (ref["iters_used"] < 20).any()          # the test exercises convergence

@@ -52,3 +52,12 @@ def test_qms_oracle_decodes():
     r = oracle.qms(H, q, 20, 15, 127, 0, early_stop=True)
     assert (r["bits"] != cw).sum() == 0
     assert (r["iters_used"] <= 20).all()
+
+
+def test_sp_oracle_early_stop():
+    H, _ = get_code("wifi648_12")
+    cw, llr = _llr(H, 32, 3.0, 13)
+    es = oracle.sp_f32(H, llr, 20, 20.0, early_stop=True)
+    full = oracle.sp_f32(H, llr, 20, 20.0)
+    assert (es["iters_used"] < 20).all() and np.array_equal(es["bits"], cw)
+    assert (full["iters_used"] == 20).all()

@@ -111,6 +111,20 @@ int ldpc_awgn_llr(const uint8_t* codeword, float* llr, int64_t B, int32_t n, flo
  * so the bits of global codeword b0+b do not depend on how a sweep is sharded.  out: device uint8 [B][k]. */
 int ldpc_random_bits(uint8_t* out, int64_t B, int32_t k, uint64_t seed, int64_t b0, void* stream);
 
+/* OFDM transmitter, the reference's modulate_bits + transmit_symbols (ofdm/ofdm_functions.py:17-35):
+ * bits[nsym * bits_per_symbol] (uint8, device) -> symbols (QPSK bits_per_symbol = 2, the reference's
+ * mapping; 16-QAM = 4, Gray per dimension, new) -> blocks of ofdm_size -> unitary IDFT -> + complex AWGN
+ * of per-dimension variance 1/(2 snr).  rx_out / tx_out: interleaved complex float [nsym][2] (tx_out may
+ * be NULL).  Noise of stream sample sym0 + i is keyed by (seed, sym0 + i). nsym % ofdm_size == 0. */
+int ldpc_ofdm_tx(const uint8_t* bits, int64_t nsym, int32_t ofdm_size, int32_t bits_per_symbol, float snr,
+                 uint64_t seed, int64_t sym0, float* rx_out, float* tx_out, void* stream);
+
+/* OFDM receiver, the reference's demodulate_signal (ofdm_functions.py:63-78): unitary DFT per block,
+ * LLR = log P(1)/P(0) per bit with noise_power 0.5/snr (QPSK: the reference's closed form; 16-QAM:
+ * exact log-sum-exp).  llr_out: float [nsym * bits_per_symbol]; sym_out (may be NULL): [nsym][2]. */
+int ldpc_ofdm_demod(const float* rx, int64_t nsym, int32_t ofdm_size, int32_t bits_per_symbol, float snr,
+                    float* llr_out, float* sym_out, void* stream);
+
 const char* ldpc_last_error(void);
 int ldpc_device_count(void);
 const char* ldpc_version(void);

@@ -5,7 +5,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRCS = ["abi.hip", "generic.hip", "qc.hip"]
+SRCS = ["abi.hip", "generic.hip", "qc.hip", "channel.hip"]
 OUT = os.path.join(HERE, "ldpc_amd", "libldpc_hip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off",  # min-sum must round exactly like oracle/ldpc_oracle.c (no FMA contraction)

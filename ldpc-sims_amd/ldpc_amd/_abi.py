@@ -20,7 +20,8 @@ F_EARLY_STOP, F_DEVICE_PTRS, F_F64, F_SOFT_Z, F_FORCE_GENERIC = 1, 2, 4, 8, 16
 EXPORTS = (
     "ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
     "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
-    "ldpc_random_bits", "ldpc_last_error", "ldpc_device_count", "ldpc_version",
+    "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_last_error", "ldpc_device_count",
+    "ldpc_version",
 )
 
 
@@ -70,9 +71,11 @@ def load(path: str | None = None):
     L.ldpc_count_errors.argtypes = [vp, vp, i64, i32, i32, vp, vp]
     L.ldpc_awgn_llr.argtypes = [vp, vp, i64, i32, ctypes.c_float, ctypes.c_uint64, i64, vp]
     L.ldpc_random_bits.argtypes = [vp, i64, i32, ctypes.c_uint64, i64, vp]
+    L.ldpc_ofdm_tx.argtypes = [vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64, i64, vp, vp, vp]
+    L.ldpc_ofdm_demod.argtypes = [vp, i64, i32, i32, ctypes.c_float, vp, vp, vp]
     for f in ("ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
               "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
-              "ldpc_random_bits", "ldpc_device_count"):
+              "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_device_count"):
         getattr(L, f).restype = ctypes.c_int
     L.ldpc_last_error.restype = ctypes.c_char_p
     L.ldpc_version.restype = ctypes.c_char_p

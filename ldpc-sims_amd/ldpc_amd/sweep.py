@@ -26,14 +26,20 @@ import numpy as np
 from . import _abi
 from .api import get_decoder
 from .codes import get_code
+from .channel import ofdm_demod, ofdm_tx
 from .synth import DeviceEncoder
 from .dist import ebn0_sigma, sweep as dist_sweep
 
 
 def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=0.0, snr_db=(0.0,),
         codewords=65536, batch=65536, seed=1, rank=0, world=1, device=0, early_stop=False, qstep=1.0,
-        qmax=15, app_max=127):
-    """Returns dict(snrdb, uncoded_ber, coded_ber, coded_bler, codewords, seconds)."""
+        qmax=15, app_max=127, mod="bpsk", ofdm_size=32):
+    """Returns dict(snrdb, uncoded_ber, coded_ber, coded_bler, codewords, seconds).
+
+    ``mod``: "bpsk" (BPSK/AWGN LLRs), "qpsk-ofdm" (the reference's chain: modulate_bits, transmit_symbols,
+    demodulate_signal), "16qam-ofdm" (16-QAM Gray over OFDM, exact LLRs; not in the reference).  Points
+    are Eb/N0 in dB; the OFDM modes transmit at Es/N0 = Eb/N0 * R * bits_per_symbol (R = 1/2 QPSK:
+    Es/N0 = Eb/N0, the reference's "SNR")."""
     import torch
     H, _ = get_code(code) if isinstance(code, str) else (code, None)
     m, n = H.shape
@@ -60,7 +66,17 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
             B = min(bmax, hi - s)
             _abi.check(lib.ldpc_random_bits(info.data_ptr(), B, k, seed * 7919 + i, s, st))
             cw = enc.encode(info[:B])
-            _abi.check(lib.ldpc_awgn_llr(cw.data_ptr(), llr.data_ptr(), B, n, sigma, seed * 104729 + i, s, st))
+            if mod == "bpsk":
+                _abi.check(lib.ldpc_awgn_llr(cw.data_ptr(), llr.data_ptr(), B, n, sigma, seed * 104729 + i, s, st))
+            else:
+                bps = 2 if mod == "qpsk-ofdm" else 4
+                esn0 = 10.0 ** (snr_db[i] / 10.0) * rate * bps
+                stream = cw.view(-1)
+                blk = bps * ofdm_size
+                if stream.numel() % blk:  # pad the bit stream to whole OFDM blocks (extra symbols dropped)
+                    stream = torch.cat([stream, torch.zeros(blk - stream.numel() % blk, dtype=torch.uint8, device=dev)])
+                rx = ofdm_tx(stream, ofdm_size, bps, esn0, seed * 104729 + i, s * n // bps)
+                llr[:B].copy_(ofdm_demod(rx, ofdm_size, bps, esn0)[:B * n].view(B, n))
             unc[i] += ((llr[:B] > 0).to(torch.uint8) != cw).sum()      # (np.sign(llr)+1)//2 decisions
             _abi.check(lib.ldpc_decode_ex(dec._h, llr.data_ptr(), B, p, bits.data_ptr(), None, None,
                                           ws.data_ptr(), wsb, st))
@@ -79,7 +95,7 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
                 coded_bler=c[:, 1] / c[:, 2],
                 codewords=c[:, 2].astype(np.int64), seconds=secs,
                 config=dict(code=code if isinstance(code, str) else "custom", algo=algo, iters=iters,
-                            clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop))
+                            clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop, mod=mod))
 
 
 def save(result: dict, path: str):
@@ -112,6 +128,7 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--early-stop", action="store_true")
+    ap.add_argument("--mod", default="bpsk", choices=["bpsk", "qpsk-ofdm", "16qam-ofdm"])
     ap.add_argument("--out", default=None, help="results .json or .pkl (reference schema)")
     a = ap.parse_args(argv)
     import torch
@@ -123,7 +140,7 @@ def main(argv=None):
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     r = run(a.code, a.algo, a.iters, a.clamp, a.alpha, a.beta, _parse_points(a.snr), a.n, a.batch, a.seed,
-            rank, world, local, a.early_stop)
+            rank, world, local, a.early_stop, mod=a.mod)
     if rank == 0:
         for i, e in enumerate(r["snrdb"]):
             print(f"{e:5.2f} dB  uncoded {r['uncoded_ber'][i]:.4e}  coded BER {r['coded_ber'][i]:.4e}  "

@@ -17,8 +17,11 @@ PUB_BLER = [8.776e-1, 7.269e-1, 5.136e-1, 2.926e-1, 1.276e-1, 4.373e-2, 1.086e-2
 N = 65536
 
 
-def test_reproduces_published_curve():
-    r = run("peg64_32", "tanh", 3, 20.0, snr_db=SNR, codewords=N, batch=N, seed=11)
+@pytest.mark.parametrize("mod", ["bpsk", "qpsk-ofdm"])
+def test_reproduces_published_curve(mod):
+    """qpsk-ofdm is the reference's own channel chain (modulate_bits -> transmit_symbols ->
+    demodulate_signal, ofdm_size 32); bpsk is its distributional equivalent."""
+    r = run("peg64_32", "tanh", 3, 20.0, snr_db=SNR, codewords=N, batch=N, seed=11, mod=mod)
     assert r["codewords"].tolist() == [N] * 11
     for i in SNR:
         # two independent estimates with N codewords each: sigma of the difference, 5 sigma + 2 counts
@@ -42,3 +45,20 @@ def test_sweep_shard_independent_data():
     # without a process group each rank keeps its own counts: they must add up to the unsharded run
     tot = b0["coded_bler"] * b0["codewords"] + b1["coded_bler"] * b1["codewords"]
     assert np.allclose(tot, a["coded_bler"] * a["codewords"])
+
+
+def test_16qam_ofdm_sweep_1944_sp():
+    """BASELINE config [2]'s front end: (1944,5/6), tanh-SP, 16-QAM OFDM.  Uncoded BER matches Gray
+    16-QAM theory, (3Q(1/s) + 2Q(3/s) - Q(5/s))/4 with s = sqrt(5/(Es/N0)) in unit-level spacing;
+    the waterfall sits between Es/N0 = 9.2 dB (Eb/N0 4) and 14.2 dB (Eb/N0 9)."""
+    from scipy.special import erfc
+    pts = [4.0, 9.0]
+    r = run("wifi1944_56", "tanh", 20, 20.0, snr_db=pts, codewords=2048, batch=2048, seed=2, mod="16qam-ofdm")
+    Q = lambda x: 0.5 * erfc(x / np.sqrt(2))
+    for i, e in enumerate(pts):
+        es = 10 ** (e / 10) * (5 / 6) * 4
+        s = np.sqrt(5 / es)
+        th = (3 * Q(1 / s) + 2 * Q(3 / s) - Q(5 / s)) / 4
+        nb = 2048 * 1944
+        assert abs(r["uncoded_ber"][i] - th) < 5 * np.sqrt(th / nb) + 1e-6, (e, r["uncoded_ber"][i], th)
+    assert r["coded_bler"][0] > 0.9 and r["coded_bler"][1] < 0.05, r["coded_bler"]

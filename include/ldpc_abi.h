@@ -92,6 +92,31 @@ int ldpc_decode_ex(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_p
 int ldpc_decode(const ldpc_graph* g, const float* llr, int64_t B, int32_t iters, float clamp, int32_t algo,
                 int32_t flags, uint8_t* bits_out, float* soft_out, void* stream);
 
+/* Weighted BP — the reference module with trained (non-unit) VC weights: layers[i][0].input_weight
+ * (E x E, masked by mask_v) and llr_weight (1 x n) per iteration, final_layer[0].input_weight (n x E) and
+ * llr_weight (pytorch/bp/bp_vc.py:16-27, bp/bp.py:27-39).  Compact layout (element type = the decode
+ * precision, DEVICE pointers, any may be NULL = all ones):
+ *   vn      [iters][W]  vn[it*W + wofs[v] + t*d_v + u] = weight of var-slot u's c2v into var-slot t's v2c
+ *                       (slot = position among v's edges in ascending check order; u == t unused);
+ *                       W = sum_v d_v^2, wofs[v] = sum_{v' < v} d_v'^2
+ *   llr     [iters][n]  per-variable LLR weight of each iteration
+ *   fin     [E]         final layer: fin[var_ptr[v] + u] = weight of var-slot u into z_v
+ *   fin_llr [n]
+ * v2c = tanh(0.5 * (llr_w * L + sum_{u != t} w_tu * c2v_u)); z = 0.5 * (fin_llr * L + sum_u fin_u c2v_u).
+ * tanh sum-product only, no early stop; always runs the generic CSR kernels (query the workspace with
+ * LDPC_F_FORCE_GENERIC set). */
+typedef struct ldpc_bp_weights {
+    const void* vn;
+    const void* llr;
+    const void* fin;
+    const void* fin_llr;
+} ldpc_bp_weights;
+
+int ldpc_weights_layout(const ldpc_graph* g, int64_t* vn_per_iter, int64_t* fin_len);
+int ldpc_decode_weighted(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_params* p,
+                         const ldpc_bp_weights* w, uint8_t* bits_out, void* soft_out, int32_t* iters_used,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
 /* Error counting on device, the metrics of evaluate_quantized.py:139-141 for one SNR point:
  *   counts[0] += bit errors over the first info_bits positions of each codeword (coded BER numerator)
  *   counts[1] += codewords with any error over all n positions              (coded BLER numerator)
@@ -124,6 +149,15 @@ int ldpc_ofdm_tx(const uint8_t* bits, int64_t nsym, int32_t ofdm_size, int32_t b
  * exact log-sum-exp).  llr_out: float [nsym * bits_per_symbol]; sym_out (may be NULL): [nsym][2]. */
 int ldpc_ofdm_demod(const float* rx, int64_t nsym, int32_t ofdm_size, int32_t bits_per_symbol, float snr,
                     float* llr_out, float* sym_out, void* stream);
+
+/* ADC quantizer — replaces quantizer (pytorch/ofdm/ofdm_functions.py:37-51) and the AGC of gen_qdata
+ * (:118-128).  rx / q_out: complex64 interleaved DEVICE buffers [nsym].  Exactly one of clip_ratio (AGC:
+ * clip = std(rx) * clip_ratio computed on device over these nsym samples, as np.std of the complex
+ * signal) or clip_value (fixed clip) must be > 0.  Arithmetic in fp64 as the reference:
+ * step = 2 clip / (2^b - 1), q = clip(step * floor(x/step + .5), -(2^b/2) step + 1, (2^b/2) step - 1).
+ * clip_out (optional, device double) receives the clip used in AGC mode.  Asynchronous on stream. */
+int ldpc_adc_quantize(const float* rx, int64_t nsym, int32_t num_bits, double clip_ratio, double clip_value,
+                      float* q_out, double* clip_out, void* stream);
 
 const char* ldpc_last_error(void);
 int ldpc_device_count(void);

@@ -18,6 +18,8 @@ struct ldpc_graph {
     int m = 0, n = 0, E = 0, device = 0;
     int max_dc = 0, max_dv = 0;
     int32_t *d_row_ptr = nullptr, *d_col_idx = nullptr, *d_var_ptr = nullptr, *d_var_edges = nullptr;
+    int32_t* d_wofs = nullptr;  // weighted BP: [n+1] offsets of the per-variable d x d weight blocks
+    int64_t W = 0;
     const ldpc::QCSpec* qc = nullptr;
     std::mutex mtx;  // guards the internal workspace
     void* ws = nullptr;
@@ -146,7 +148,8 @@ static bool params_valid(const ldpc_params* p) {
 }
 
 static GenericArgs gargs(const ldpc_graph* g) {
-    return GenericArgs{g->d_row_ptr, g->d_col_idx, g->d_var_ptr, g->d_var_edges, g->m, g->n, g->E, g->max_dc, g->max_dv};
+    return GenericArgs{g->d_row_ptr, g->d_col_idx, g->d_var_ptr, g->d_var_edges, g->m, g->n, g->E, g->max_dc, g->max_dv,
+                       g->d_wofs, g->W};
 }
 
 static bool use_qc(const ldpc_graph* g, const ldpc_params* p) {
@@ -183,6 +186,15 @@ static int build_graph(ldpc_graph* g, int m, int n, const std::vector<int32_t>& 
     for (int c = 0; c < m; ++c) g->max_dc = std::max(g->max_dc, row_ptr[c + 1] - row_ptr[c]);
     g->max_dv = 0;
     for (int v = 0; v < n; ++v) g->max_dv = std::max(g->max_dv, var_ptr[v + 1] - var_ptr[v]);
+    std::vector<int32_t> wofs(n + 1, 0);
+    int64_t W = 0;
+    for (int v = 0; v < n; ++v) {
+        const int64_t d = var_ptr[v + 1] - var_ptr[v];
+        W += d * d;
+        if (W > INT32_MAX) return set_error(LDPC_EUNSUPPORTED, "weight layout exceeds int32 offsets");
+        wofs[v + 1] = (int32_t)W;
+    }
+    g->W = W;
     DeviceGuard dg(g->device);
     auto up = [](int32_t** d, const std::vector<int32_t>& h) -> hipError_t {
         hipError_t e = hipMalloc((void**)d, std::max<size_t>(4, h.size() * 4));
@@ -192,7 +204,7 @@ static int build_graph(ldpc_graph* g, int m, int n, const std::vector<int32_t>& 
     hipError_t e;
     if ((e = up(&g->d_row_ptr, row_ptr)) != hipSuccess || (e = up(&g->d_col_idx, col_idx)) != hipSuccess ||
         (e = up(&g->d_var_ptr, var_ptr)) != hipSuccess ||
-        (e = up(&g->d_var_edges, var_edges)) != hipSuccess)
+        (e = up(&g->d_var_edges, var_edges)) != hipSuccess || (e = up(&g->d_wofs, wofs)) != hipSuccess)
         return set_error(e == hipErrorOutOfMemory ? LDPC_ENOMEM : LDPC_EHIP, "graph upload: %s", hipGetErrorString(e));
     return LDPC_OK;
 }
@@ -296,6 +308,7 @@ int ldpc_graph_destroy(ldpc_graph* g) {
     (void)hipFree(g->d_col_idx);
     (void)hipFree(g->d_var_ptr);
     (void)hipFree(g->d_var_edges);
+    (void)hipFree(g->d_wofs);
     if (g->ws) (void)hipFree(g->ws);
     delete g;
     return LDPC_OK;
@@ -316,8 +329,9 @@ int ldpc_workspace_size(const ldpc_graph* g, int64_t B, const ldpc_params* p, si
     return LDPC_OK;
 }
 
-int ldpc_decode_ex(const ldpc_graph* gc, const void* llr, int64_t B, const ldpc_params* p, uint8_t* bits_out,
-                   void* soft_out, int32_t* iters_used, void* workspace, size_t workspace_bytes, void* stream) {
+static int decode_impl(const ldpc_graph* gc, const void* llr, int64_t B, const ldpc_params* p, uint8_t* bits_out,
+                       void* soft_out, int32_t* iters_used, void* workspace, size_t workspace_bytes, void* stream,
+                       const BPWeights* w) {
     ldpc_graph* g = const_cast<ldpc_graph*>(gc);
     if (!g) return set_error(LDPC_EINVAL, "null graph");
     if (!params_valid(p)) return set_error(LDPC_EINVAL, "invalid ldpc_params");
@@ -369,7 +383,7 @@ int ldpc_decode_ex(const ldpc_graph* gc, const void* llr, int64_t B, const ldpc_
     if (use_qc(g, p)) {
         rc = qc_decode(g->qc, llr_d, B, *p, bits_d, soft_d, used_d, ws, st);
     } else {
-        rc = generic_decode(gargs(g), llr_d, B, *p, bits_d, soft_d, used_d, ws, st);
+        rc = generic_decode(gargs(g), llr_d, B, *p, bits_d, soft_d, used_d, ws, st, w);
     }
     if (rc != LDPC_OK) return rc;
     if (!dev) {
@@ -384,6 +398,30 @@ int ldpc_decode_ex(const ldpc_graph* gc, const void* llr, int64_t B, const ldpc_
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return set_error(LDPC_EHIP, "decode: %s", hipGetErrorString(e));
     }
     return LDPC_OK;
+}
+
+int ldpc_decode_ex(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_params* p, uint8_t* bits_out,
+                   void* soft_out, int32_t* iters_used, void* workspace, size_t workspace_bytes, void* stream) {
+    return decode_impl(g, llr, B, p, bits_out, soft_out, iters_used, workspace, workspace_bytes, stream, nullptr);
+}
+
+int ldpc_weights_layout(const ldpc_graph* g, int64_t* vn_per_iter, int64_t* fin_len) {
+    if (!g) return set_error(LDPC_EINVAL, "null graph");
+    if (vn_per_iter) *vn_per_iter = g->W;
+    if (fin_len) *fin_len = g->E;
+    return LDPC_OK;
+}
+
+int ldpc_decode_weighted(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_params* p,
+                         const ldpc_bp_weights* w, uint8_t* bits_out, void* soft_out, int32_t* iters_used,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+    if (!p || !params_valid(p)) return set_error(LDPC_EINVAL, "invalid ldpc_params");
+    if (p->algo != LDPC_ALGO_TANH_SP || (p->flags & LDPC_F_EARLY_STOP))
+        return set_error(LDPC_EUNSUPPORTED, "weighted BP is tanh sum-product without early stop");
+    ldpc_params q = *p;
+    q.flags |= LDPC_F_FORCE_GENERIC;
+    const BPWeights bw{w ? w->vn : nullptr, w ? w->llr : nullptr, w ? w->fin : nullptr, w ? w->fin_llr : nullptr};
+    return decode_impl(g, llr, B, &q, bits_out, soft_out, iters_used, workspace, workspace_bytes, stream, &bw);
 }
 
 int ldpc_decode(const ldpc_graph* g, const float* llr, int64_t B, int32_t iters, float clamp, int32_t algo,

@@ -118,6 +118,70 @@ __global__ __launch_bounds__(256) void k_ofdm_demod(const float2* __restrict__ r
     }
 }
 
+// ---- ADC quantizer (quantizer / gen_qdata, ofdm_functions.py:37-51,118-128) ----
+// AGC: sigma = np.std(rx) over the complex stream = sqrt(mean |x - mean x|^2), in fp64, deterministic
+// (fixed grid of partial sums reduced in a fixed order by one workgroup).
+constexpr int kMomBlocks = 512;
+
+__global__ __launch_bounds__(256) void k_moments(const float2* __restrict__ x, int64_t n, double* __restrict__ part) {
+    __shared__ double sh[3][256];
+    double sr = 0.0, si = 0.0, sq = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float2 v = x[i];
+        sr += v.x;
+        si += v.y;
+        sq += (double)v.x * v.x + (double)v.y * v.y;
+    }
+    sh[0][threadIdx.x] = sr;
+    sh[1][threadIdx.x] = si;
+    sh[2][threadIdx.x] = sq;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            for (int c = 0; c < 3; ++c) sh[c][threadIdx.x] += sh[c][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) part[blockIdx.x * 3 + threadIdx.x] = sh[threadIdx.x][0];
+}
+
+// part[kMomBlocks][3] -> part[0] = clip = sigma * clip_ratio
+__global__ __launch_bounds__(256) void k_agc_clip(double* __restrict__ part, int64_t n, double clip_ratio) {
+    __shared__ double sh[3][256];
+    for (int c = 0; c < 3; ++c) {
+        double a = 0.0;
+        for (int b = threadIdx.x; b < kMomBlocks; b += 256) a += part[b * 3 + c];
+        sh[c][threadIdx.x] = a;
+    }
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            for (int c = 0; c < 3; ++c) sh[c][threadIdx.x] += sh[c][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double mr = sh[0][0] / n, mi = sh[1][0] / n;
+        const double var = fmax(sh[2][0] / n - (mr * mr + mi * mi), 0.0);
+        part[0] = sqrt(var) * clip_ratio;
+    }
+}
+
+// q = clip(step * floor(x / step + .5), -(L/2) step + 1, (L/2) step - 1), step = 2 clip / (L - 1), in fp64
+// exactly as written (the +-1 in the bounds mixes units, ofdm_functions.py:44-45; lo > hi gives hi, as
+// np.clip does).  clip comes from the device (AGC) when clip_dev != nullptr.
+__global__ __launch_bounds__(256) void k_adc(const float2* __restrict__ x, int64_t n, int nbits, double clip_host,
+                                             const double* __restrict__ clip_dev, float2* __restrict__ q) {
+    const double clip = clip_dev ? clip_dev[0] : clip_host;
+    const double L = (double)(1ll << nbits);
+    const double step = 2.0 * clip / (L - 1.0);
+    const double lo = -(L / 2.0) * step + 1.0, hi = (L / 2.0) * step - 1.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float2 v = x[i];
+        const double re = fmin(fmax(step * floor((double)v.x / step + 0.5), lo), hi);
+        const double im = fmin(fmax(step * floor((double)v.y / step + 0.5), lo), hi);
+        q[i] = make_float2((float)re, (float)im);
+    }
+}
+
 }  // namespace ldpc
 
 using namespace ldpc;
@@ -156,6 +220,29 @@ int ldpc_ofdm_demod(const float* rx, int64_t nsym, int32_t ofdm_size, int32_t bi
                                                                                  bits_per_symbol, snr, llr_out, (float2*)sym_out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "ofdm_demod: %s", hipGetErrorString(e));
+    return LDPC_OK;
+}
+
+int ldpc_adc_quantize(const float* rx, int64_t nsym, int32_t num_bits, double clip_ratio, double clip_value,
+                      float* q_out, double* clip_out, void* stream) {
+    if (!rx || !q_out || nsym < 0 || num_bits < 1 || num_bits > 24 || (clip_ratio > 0.0) == (clip_value > 0.0))
+        return set_error(LDPC_EINVAL, "bad adc_quantize arguments (exactly one of clip_ratio / clip_value must be > 0)");
+    if (nsym == 0) return LDPC_OK;
+    hipStream_t st = (hipStream_t)stream;
+    double* part = nullptr;
+    if (clip_ratio > 0.0) {
+        if (hipMallocAsync((void**)&part, sizeof(double) * 3 * kMomBlocks, st) != hipSuccess)
+            return set_error(LDPC_ENOMEM, "adc_quantize: scratch allocation failed");
+        k_moments<<<kMomBlocks, 256, 0, st>>>((const float2*)rx, nsym, part);
+        k_agc_clip<<<1, 256, 0, st>>>(part, nsym, clip_ratio);
+        if (clip_out) (void)hipMemcpyAsync(clip_out, part, sizeof(double), hipMemcpyDeviceToDevice, st);
+    }
+    const int64_t want = (nsym + 255) / 256;
+    const unsigned grid = (unsigned)(want < 8192 ? want : 8192);
+    k_adc<<<grid, 256, 0, st>>>((const float2*)rx, nsym, num_bits, clip_value, part, (float2*)q_out);
+    if (part) (void)hipFreeAsync(part, st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(LDPC_EHIP, "adc_quantize: %s", hipGetErrorString(e));
     return LDPC_OK;
 }
 

@@ -73,10 +73,17 @@ int fill_i32(int32_t* p, int64_t count, int32_t value, hipStream_t st);
 struct GenericArgs {
     const int32_t *row_ptr, *col_idx, *var_ptr, *var_edges;
     int m, n, E, max_dc, max_dv;
+    const int32_t* wofs;  // [n+1] start of variable v's d_v x d_v block in one iteration's compact VN weights
+    int64_t W;            // sum_v d_v^2
+};
+// Weighted BP (bp_vc.py:16-27 with non-unit weights): device arrays of the decode precision, any may be
+// null (= all ones).  vn [iters][W], lw [iters][n], fin [E] (var-slot order), flw [n].
+struct BPWeights {
+    const void *vn, *lw, *fin, *flw;
 };
 size_t generic_workspace(const GenericArgs& g, int64_t B, const ldpc_params& p);
 int generic_decode(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,
-                   void* soft, int32_t* iters_used, char* ws, hipStream_t st);
+                   void* soft, int32_t* iters_used, char* ws, hipStream_t st, const BPWeights* w = nullptr);
 
 // Structure-specialised (quasi-cyclic) decoders compiled into the library (qc.hip).
 struct QCSpec;

@@ -209,6 +209,53 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
     }
 }
 
+// Weighted VC + tanh (bp_vc.py:16-27 with input_weight / llr_weight != 1): every target slot sums its own
+// weighted sources, ascending, skipping itself — the masked mm's terms in its k order.  Weights are
+// wave-uniform (scalar loads).  vn_it/lw_it point at this iteration's block (null = ones).
+template <typename T, int MAXD>
+__global__ __launch_bounds__(256) void k_vn_spw(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
+                                                const int32_t* __restrict__ wofs, const T* __restrict__ vn_it,
+                                                const T* __restrict__ lw_it, const T* __restrict__ L,
+                                                const T* __restrict__ c2v, T* __restrict__ v2c, int64_t B, int64_t ldb,
+                                                int first) {
+    constexpr int V = VW<T, MAXD>::value;
+    const int v = blockIdx.y;
+    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
+    if (cw >= B) return;
+    const int a = var_ptr[v];
+    const int d = var_ptr[v + 1] - a;
+    if (d == 0) return;
+    const T* wv = vn_it ? vn_it + wofs[v] : nullptr;
+    const T lw = lw_it ? lw_it[v] : T(1);
+    const Vec<T, V> Lv = vload<T, V>(L + (int64_t)v * ldb + cw);
+    Vec<T, V> x[MAXD];
+    int64_t off[MAXD];
+#pragma unroll
+    for (int k = 0; k < MAXD; ++k) {
+        off[k] = (int64_t)var_edges[a + (k < d ? k : d - 1)] * ldb + cw;
+        if (first) {
+#pragma unroll
+            for (int i = 0; i < V; ++i) x[k].x[i] = T(0);
+        } else {
+            x[k] = vload<T, V>(c2v + off[k]);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < MAXD; ++t)
+        if (t < d) {
+            Vec<T, V> o;
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                T S = T(0);
+#pragma unroll
+                for (int u = 0; u < MAXD; ++u)
+                    if (u < d && u != t) S += (wv ? wv[t * d + u] : T(1)) * x[u].x[i];
+                o.x[i] = Num<T>::tanh_(T(0.5) * (lw * Lv.x[i] + S));
+            }
+            vstore<T, V>(v2c + off[t], o);
+        }
+}
+
 template <typename T, int MAXD, bool ES>
 __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_ptr, const T* __restrict__ v2c,
                                                T* __restrict__ c2v, int64_t B, int64_t ldb, T clamp,
@@ -348,7 +395,7 @@ template <typename T, int MAXD, bool MS>
 __global__ __launch_bounds__(256) void k_final(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                const T* __restrict__ L, const T* __restrict__ c2v, int64_t B,
                                                int64_t ldb, int n, uint8_t* __restrict__ bits, T* __restrict__ soft,
-                                               int soft_z) {
+                                               int soft_z, const T* __restrict__ fin, const T* __restrict__ flw) {
     __shared__ T zt[64][65];
     const int64_t cw0 = (int64_t)blockIdx.x * 64;
     const int v0 = blockIdx.y * 64;
@@ -367,8 +414,9 @@ __global__ __launch_bounds__(256) void k_final(const int32_t* __restrict__ var_p
                 z = T(0.5) * app;
             } else {
                 T S = T(0);
-                for (int k = 0; k < d; ++k) S += c2v[(int64_t)var_edges[a + k] * ldb + cw];
-                z = T(0.5) * (Lv + S);
+                for (int k = 0; k < d; ++k)
+                    S += (fin ? fin[a + k] : T(1)) * c2v[(int64_t)var_edges[a + k] * ldb + cw];
+                z = T(0.5) * ((flw ? flw[v] : T(1)) * Lv + S);
             }
             zt[vr][tx] = z;
         }
@@ -430,7 +478,7 @@ size_t generic_workspace(const GenericArgs& g, int64_t B, const ldpc_params& p) 
 // syndrome of APP_it and the convergence update between them), then the final decision kernel.
 template <typename T, bool MS, bool ES>
 static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits, T* soft,
-               int32_t* iters_used, char* ws, hipStream_t st) {
+               int32_t* iters_used, char* ws, hipStream_t st, const BPWeights* wts) {
     const int64_t ldb = (B + 63) / 64 * 64;
     const WsLayout w = layout(g, B, sizeof(T), ES);
     T* L = (T*)(ws + w.L);
@@ -452,8 +500,19 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     }
     const int dv = pick_maxd(g.max_dv), dc = pick_maxd(g.max_dc);
     if (dv < 0 || dc < 0) return set_error(LDPC_EUNSUPPORTED, "node degree > 32 not supported by generic kernels");
+    const T* w_vn = wts ? (const T*)wts->vn : nullptr;
+    const T* w_lw = wts ? (const T*)wts->lw : nullptr;
     for (int it = 0; it < p.iters; ++it) {
         const int first = (it == 0);
+        if (!MS && wts) {
+            const T* vn_it = w_vn ? w_vn + (int64_t)it * g.W : nullptr;
+            const T* lw_it = w_lw ? w_lw + (int64_t)it * g.n : nullptr;
+#define VNW(D)                                                                                                      \
+    k_vn_spw<T, D><<<dim3(gxv(VW<T, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, g.wofs, vn_it, lw_it, L, \
+                                                                 c2v, v2c, B, ldb, first)
+            switch (dv) { case 4: VNW(4); break; case 8: VNW(8); break; case 12: VNW(12); break; case 16: VNW(16); break; case 20: VNW(20); break; case 24: VNW(24); break; default: VNW(32); }
+#undef VNW
+        } else {
 #define VN(D)                                                                                                      \
     do {                                                                                                           \
         if constexpr (MS)                                                                                          \
@@ -465,6 +524,7 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     } while (0)
         switch (dv) { case 4: VN(4); break; case 8: VN(8); break; case 12: VN(12); break; case 16: VN(16); break; case 20: VN(20); break; case 24: VN(24); break; default: VN(32); }
 #undef VN
+        }
         if (ES && it > 0) {  // the oracle tests the syndrome of APP after each iteration >= 1
             k_syndrome<<<dim3((unsigned)((B + 4 * kTB - 1) / (4 * kTB)), g.m), tb, 0, st>>>(g.row_ptr, g.col_idx, hb,
                                                                                           done, unsat, B, ldb);
@@ -483,7 +543,9 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     }
     if (p.iters == 0) (void)hipMemsetAsync(c2v, 0, sizeof(T) * (size_t)g.E * ldb, st);
     k_final<T, 32, MS><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, B,
-                                                                                      ldb, g.n, bits, soft, soft_z);
+                                                                                      ldb, g.n, bits, soft, soft_z,
+                                                                                      wts ? (const T*)wts->fin : nullptr,
+                                                                                      wts ? (const T*)wts->flw : nullptr);
     if (ES) {
         k_used_final<<<gcw, tb, 0, st>>>(done, used, B, p.iters);
     } else if (iters_used) {
@@ -493,24 +555,26 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
 }
 
 int generic_decode(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,
-                   void* soft, int32_t* iters_used, char* ws, hipStream_t st) {
+                   void* soft, int32_t* iters_used, char* ws, hipStream_t st, const BPWeights* w) {
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
+    if (w && (p.algo != LDPC_ALGO_TANH_SP || es))
+        return set_error(LDPC_EUNSUPPORTED, "weighted BP is tanh sum-product without early stop");
     int rc;
     if (p.algo == LDPC_ALGO_TANH_SP) {
         if (p.flags & LDPC_F_F64) {
             const double* x = (const double*)llr_dev;
-            rc = es ? run<double, false, true>(g, x, B, p, bits, (double*)soft, iters_used, ws, st)
-                    : run<double, false, false>(g, x, B, p, bits, (double*)soft, iters_used, ws, st);
+            rc = es ? run<double, false, true>(g, x, B, p, bits, (double*)soft, iters_used, ws, st, w)
+                    : run<double, false, false>(g, x, B, p, bits, (double*)soft, iters_used, ws, st, w);
         } else {
             const float* x = (const float*)llr_dev;
-            rc = es ? run<float, false, true>(g, x, B, p, bits, (float*)soft, iters_used, ws, st)
-                    : run<float, false, false>(g, x, B, p, bits, (float*)soft, iters_used, ws, st);
+            rc = es ? run<float, false, true>(g, x, B, p, bits, (float*)soft, iters_used, ws, st, w)
+                    : run<float, false, false>(g, x, B, p, bits, (float*)soft, iters_used, ws, st, w);
         }
     } else if (p.algo == LDPC_ALGO_MIN_SUM) {
         if (p.flags & LDPC_F_F64) return set_error(LDPC_EUNSUPPORTED, "min-sum is float32 only");
         const float* x = (const float*)llr_dev;
-        rc = es ? run<float, true, true>(g, x, B, p, bits, (float*)soft, iters_used, ws, st)
-                : run<float, true, false>(g, x, B, p, bits, (float*)soft, iters_used, ws, st);
+        rc = es ? run<float, true, true>(g, x, B, p, bits, (float*)soft, iters_used, ws, st, w)
+                : run<float, true, false>(g, x, B, p, bits, (float*)soft, iters_used, ws, st, w);
     } else {
         return set_error(LDPC_EUNSUPPORTED, "algo %d not supported by the generic kernels", p.algo);
     }

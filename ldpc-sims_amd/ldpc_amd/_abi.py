@@ -20,7 +20,8 @@ F_EARLY_STOP, F_DEVICE_PTRS, F_F64, F_SOFT_Z, F_FORCE_GENERIC = 1, 2, 4, 8, 16
 EXPORTS = (
     "ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
     "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
-    "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_last_error", "ldpc_device_count",
+    "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_adc_quantize", "ldpc_weights_layout",
+    "ldpc_decode_weighted", "ldpc_last_error", "ldpc_device_count",
     "ldpc_version",
 )
 
@@ -37,6 +38,12 @@ class Params(ctypes.Structure):
     _fields_ = [("iters", ctypes.c_int32), ("algo", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("clamp", ctypes.c_float), ("alpha", ctypes.c_float), ("beta", ctypes.c_float),
                 ("qmax", ctypes.c_int32), ("app_max", ctypes.c_int32), ("qstep", ctypes.c_float)]
+
+
+class BPWeights(ctypes.Structure):
+    """ldpc_bp_weights: device pointers (vn, llr, fin, fin_llr), NULL = all ones."""
+    _fields_ = [("vn", ctypes.c_void_p), ("llr", ctypes.c_void_p), ("fin", ctypes.c_void_p),
+                ("fin_llr", ctypes.c_void_p)]
 
 
 _lib = None
@@ -73,9 +80,14 @@ def load(path: str | None = None):
     L.ldpc_random_bits.argtypes = [vp, i64, i32, ctypes.c_uint64, i64, vp]
     L.ldpc_ofdm_tx.argtypes = [vp, i64, i32, i32, ctypes.c_float, ctypes.c_uint64, i64, vp, vp, vp]
     L.ldpc_ofdm_demod.argtypes = [vp, i64, i32, i32, ctypes.c_float, vp, vp, vp]
+    L.ldpc_adc_quantize.argtypes = [vp, i64, i32, ctypes.c_double, ctypes.c_double, vp, vp, vp]
+    L.ldpc_weights_layout.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    L.ldpc_decode_weighted.argtypes = [vp, vp, i64, ctypes.POINTER(Params), ctypes.POINTER(BPWeights), vp, vp, vp,
+                                       vp, sz, vp]
     for f in ("ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
               "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
-              "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_device_count"):
+              "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_adc_quantize", "ldpc_weights_layout", "ldpc_decode_weighted",
+              "ldpc_device_count"):
         getattr(L, f).restype = ctypes.c_int
     L.ldpc_last_error.restype = ctypes.c_char_p
     L.ldpc_version.restype = ctypes.c_char_p

@@ -50,6 +50,10 @@ class Decoder:
         z = ctypes.c_int32()
         check(self.lib.ldpc_graph_info(self._h, None, None, None, ctypes.byref(z)))
         self.qc_z = int(z.value)
+        w, f = ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.ldpc_weights_layout(self._h, ctypes.byref(w), ctypes.byref(f)))
+        self.weights_per_iter = int(w.value)   # compact VN weights per iteration (sum_v d_v^2)
+        self.graph = g
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -81,17 +85,47 @@ class Decoder:
         check(self.lib.ldpc_workspace_size(self._h, int(B), ctypes.byref(p), ctypes.byref(out)))
         return int(out.value)
 
+    def device_weights(self, weights, iters: int, precision="f32"):
+        """Compact weights (dict vn [iters][W], llr [iters][n], fin [E], fin_llr [n]; numpy or torch; any key
+        None/missing = ones) -> (BPWeights struct, device tensors kept alive).  Shapes are checked here."""
+        torch = _torch()
+        tdt = torch.float64 if precision == "f64" else torch.float32
+        dev = torch.device("cuda", self.device)
+        shapes = dict(vn=(iters, self.weights_per_iter), llr=(iters, self.n), fin=(self.E,), fin_llr=(self.n,))
+        keep, ptrs = [], []
+        for k in ("vn", "llr", "fin", "fin_llr"):
+            a = (weights or {}).get(k)
+            if a is None:
+                ptrs.append(None)
+                continue
+            t = torch.as_tensor(a).detach().to(device=dev, dtype=tdt).contiguous()
+            if tuple(t.shape) != shapes[k]:
+                raise ValueError(f"weights[{k!r}] must have shape {shapes[k]}, got {tuple(t.shape)}")
+            keep.append(t)
+            ptrs.append(t.data_ptr())
+        return _abi.BPWeights(*ptrs), keep
+
     def decode(self, llr, iters: int, *, algo="tanh", clamp=10.0, alpha=1.0, beta=0.0, early_stop=False,
                precision="f32", soft=None, qmax=15, app_max=127, qstep=1.0, force_generic=False, stream=None,
-               want_bits=True, want_iters=False):
+               want_bits=True, want_iters=False, weights=None):
         """Decode a (B, n) batch of LLRs (log P1/P0).  numpy in -> numpy out (host staging inside the
         library); torch GPU tensor in -> torch GPU tensors out, asynchronous on ``stream`` (default: the
-        current torch stream) with a torch-allocated workspace.  Returns dict(bits, soft, iters_used)."""
+        current torch stream) with a torch-allocated workspace.  Returns dict(bits, soft, iters_used).
+        ``weights``: weighted BP (tanh-SP only), compact layout of ``Graph.compact_weights``."""
         is_torch = type(llr).__module__.startswith("torch")
         on_gpu = is_torch and llr.is_cuda
         fdt = np.float64 if precision == "f64" else np.float32
+        if weights is not None:
+            force_generic = True
         p = self.params(iters, algo, clamp, alpha, beta, early_stop, precision, soft or "p1", qmax, app_max,
                         qstep, force_generic, device_ptrs=on_gpu)
+        wstruct, _wkeep = (self.device_weights(weights, iters, precision) if weights is not None else (None, None))
+
+        def call(*args):
+            if wstruct is None:
+                return self.lib.ldpc_decode_ex(self._h, args[0], args[1], ctypes.byref(p), *args[2:])
+            return self.lib.ldpc_decode_weighted(self._h, args[0], args[1], ctypes.byref(p), ctypes.byref(wstruct),
+                                                 *args[2:])
         if on_gpu:
             torch = _torch()
             tdt = torch.float64 if precision == "f64" else torch.float32
@@ -106,11 +140,9 @@ class Decoder:
             wsb = self.workspace_bytes(B, p)
             ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dev)
             st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-            check(self.lib.ldpc_decode_ex(self._h, x.data_ptr(), B, ctypes.byref(p),
-                                          bits.data_ptr() if bits is not None else None,
-                                          sft.data_ptr() if sft is not None else None,
-                                          used.data_ptr() if used is not None else None, ws.data_ptr(), wsb,
-                                          ctypes.c_void_p(st)))
+            check(call(x.data_ptr(), B, bits.data_ptr() if bits is not None else None,
+                       sft.data_ptr() if sft is not None else None,
+                       used.data_ptr() if used is not None else None, ws.data_ptr(), wsb, ctypes.c_void_p(st)))
             # ws was allocated on the current stream; returning it keeps it alive until the caller drops the
             # result (torch's allocator then recycles it in stream order).
             return dict(bits=bits, soft=sft, iters_used=used, workspace=ws)
@@ -123,10 +155,11 @@ class Decoder:
         bits = np.empty((B, self.n), np.uint8) if want_bits else None
         sft = np.empty((B, self.n), fdt) if soft else None
         used = np.empty((B,), np.int32) if want_iters else None
-        check(self.lib.ldpc_decode_ex(self._h, x.ctypes.data, B, ctypes.byref(p),
-                                      bits.ctypes.data if bits is not None else None,
-                                      sft.ctypes.data if sft is not None else None,
-                                      used.ctypes.data if used is not None else None, None, 0, None))
+        if wstruct is not None:  # the weights were uploaded on the current torch stream; the library uses 0
+            _torch().cuda.synchronize(self.device)
+        check(call(x.ctypes.data, B, bits.ctypes.data if bits is not None else None,
+                   sft.ctypes.data if sft is not None else None,
+                   used.ctypes.data if used is not None else None, None, 0, None))
         return dict(bits=bits, soft=sft, iters_used=used)
 
 
@@ -203,17 +236,49 @@ def _make_bp_module():
         """``bp/bp.py:19-62`` interface: ``BeliefPropagation(H, iterations)``, ``forward(x, llr, clamp)``
         returns ``p1 = 1 - sigmoid(z)`` (B, n); ``.double()`` switches to float64 arithmetic like the
         reference module; ``layer_size()`` = number of edges E.  ``x`` (initial c2v messages, check-order)
-        must be zero, which is what every reference caller passes (``ofdm_functions.py:157``)."""
+        must be zero, which is what every reference caller passes (``ofdm_functions.py:157``).
+
+        Weighted ("neural") BP forward: ``set_weights(...)`` with the reference's dense per-layer
+        ``input_weight`` / ``llr_weight`` tensors, or ``load_reference_state_dict(sd)`` with a reference
+        module's ``state_dict()`` (keys ``layers.{i}.0.input_weight``, ``layers.{i}.0.llr_weight``,
+        ``final_layer.0.input_weight``, ``final_layer.0.llr_weight``, ``bp_vc.py:99-107``).  They are kept
+        in the compact layout (``Graph.compact_weights``); forward then runs the weighted kernels.
+        Training (the autograd backward of ``bp_vc.py:34-58``) is out of scope."""
 
         def __init__(self, H, iterations):
             super().__init__()
-            self.H = np.asarray(H)
+            self.H = H if isinstance(H, SparseCode) else np.asarray(H)
             self.iterations = int(iterations)
-            self.layer_size_val = int(np.count_nonzero(self.H))
+            self.graph = Graph.from_H(self.H)
+            self.layer_size_val = self.graph.E
             self.register_buffer("_dtype_probe", torch.zeros(1, dtype=torch.float32))
+            self.weights = None
 
         def layer_size(self):
             return self.layer_size_val
+
+        def set_weights(self, input_weights=None, llr_weights=None, final_input_weight=None, final_llr_weight=None):
+            """Dense reference-layout weights (lists over iterations for the first two); None = ones."""
+            def cvt(a):
+                return None if a is None else (a.detach().cpu().double().numpy() if torch.is_tensor(a) else a)
+            iw = None if input_weights is None else [cvt(a) for a in input_weights]
+            lw = None if llr_weights is None else [cvt(a) for a in llr_weights]
+            for seq in (iw, lw):
+                if seq is not None and len(seq) != self.iterations:
+                    raise ValueError(f"need {self.iterations} per-layer weights, got {len(seq)}")
+            c = self.graph.compact_weights(iw, lw, cvt(final_input_weight), cvt(final_llr_weight))
+            self.weights = {k: (None if v is None else torch.from_numpy(v)) for k, v in c.items()}
+            return self
+
+        def load_reference_state_dict(self, sd):
+            """Weights from a reference ``BeliefPropagation.state_dict()`` (load it with
+            ``torch.load(path, weights_only=True)``)."""
+            it = range(self.iterations)
+            iw = [sd.get(f"layers.{i}.0.input_weight") for i in it]
+            lw = [sd.get(f"layers.{i}.0.llr_weight") for i in it]
+            return self.set_weights(None if any(a is None for a in iw) else iw,
+                                    None if any(a is None for a in lw) else lw,
+                                    sd.get("final_layer.0.input_weight"), sd.get("final_layer.0.llr_weight"))
 
         def forward(self, x, llr, clamp_value):
             if x is not None and bool(torch.count_nonzero(x)):
@@ -222,7 +287,7 @@ def _make_bp_module():
             dev = llr.device.index if llr.is_cuda else (torch.cuda.current_device() if torch.cuda.is_available() else 0)
             d = get_decoder(self.H, dev or 0)
             r = d.decode(llr, self.iterations, algo="tanh", clamp=float(clamp_value), precision=precision,
-                         soft="p1", want_bits=False)
+                         soft="p1", want_bits=False, weights=self.weights)
             p1 = r["soft"]
             if not llr.is_cuda:
                 p1 = torch.from_numpy(p1)

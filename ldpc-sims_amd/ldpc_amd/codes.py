@@ -224,6 +224,55 @@ class Graph:
     def var_degrees(self) -> np.ndarray:
         return np.diff(self.var_ptr)
 
+    # ---- weighted BP (bp_vc.py:16-27 with non-unit input_weight / llr_weight) -------------------------
+    def weight_offsets(self) -> np.ndarray:
+        """wofs[n+1]: start of variable v's d_v x d_v block in one iteration's compact VN weights."""
+        d = self.var_degrees().astype(np.int64)
+        return np.concatenate([[0], np.cumsum(d * d)])
+
+    def vn_weight_index(self):
+        """(target var-order edge, source check-order edge, compact position) of every off-diagonal entry:
+        compact[wofs[v] + t*d + u] = input_weight[var_ptr[v]+t][var_edges[var_ptr[v]+u]] (the reference's
+        mask_v rows are var-order ids, columns check-order ids, masking.py:101-113)."""
+        wofs = self.weight_offsets()
+        tgt, src, pos = [], [], []
+        for v in range(self.n):
+            a, b = int(self.var_ptr[v]), int(self.var_ptr[v + 1])
+            d = b - a
+            for t in range(d):
+                for u in range(d):
+                    if u != t:
+                        tgt.append(a + t)
+                        src.append(int(self.var_edges[a + u]))
+                        pos.append(int(wofs[v]) + t * d + u)
+        return np.array(tgt, np.int64), np.array(src, np.int64), np.array(pos, np.int64)
+
+    def compact_weights(self, input_weights=None, llr_weights=None, final_input_weight=None,
+                        final_llr_weight=None, iters=None):
+        """Dense reference weights -> the compact layout the kernels and the oracle read.
+
+        input_weights: per-iteration E x E (the reference's ``layers[i][0].input_weight``, var-order rows,
+        check-order columns); llr_weights: per-iteration (1, n); final_input_weight: n x E
+        (``final_layer[0].input_weight``); final_llr_weight: (1, n).  Missing = all ones (returned as None).
+        """
+        out = dict(vn=None, llr=None, fin=None, fin_llr=None)
+        if input_weights is not None:
+            tgt, src, pos = self.vn_weight_index()
+            W = int(self.weight_offsets()[-1])
+            vn = np.zeros((len(input_weights), W), np.float64)
+            for i, w in enumerate(input_weights):
+                vn[i, pos] = np.asarray(w, np.float64)[tgt, src]
+            out["vn"] = vn
+        if llr_weights is not None:
+            out["llr"] = np.stack([np.asarray(w, np.float64).reshape(-1) for w in llr_weights])
+        if final_input_weight is not None:
+            fw = np.asarray(final_input_weight, np.float64)
+            vv = np.repeat(np.arange(self.n), self.var_degrees())
+            out["fin"] = fw[vv, self.var_edges]
+        if final_llr_weight is not None:
+            out["fin_llr"] = np.asarray(final_llr_weight, np.float64).reshape(-1)
+        return out
+
 
 # ---------------------------------------------------------------------------------------------
 def _gf2_solve_right(B: np.ndarray, A: np.ndarray) -> np.ndarray:

@@ -50,6 +50,18 @@ typedef struct {
     const int32_t *row_ptr, *col_idx, *var_ptr, *var_edges;
 } graph_t;
 
+/* Weighted BP (bp_vc.py:16-27 with non-unit input_weight / llr_weight): compact layout, per iteration
+ *   vn[it*W + wofs[v] + t*d_v + u]  weight of var-slot u's c2v into var-slot t's v2c (u != t; slot = position in
+ *                                   var_edges, ascending check), W = sum_v d_v^2, wofs[v] = sum_{v'<v} d_v'^2
+ *   lw[it*n + v]                    llr_weight of variable v
+ *   fin[var_ptr[v] + u], flw[v]     the final layer's weights
+ * v2c = 0.5 * (lw*L + sum_{u != t, ascending} w_tu * x_u) — the masked mm of bp_vc.py:19 and :24,27. */
+typedef struct {
+    const void *vn, *lw, *fin, *flw;
+    const int64_t* wofs;
+    int64_t W;
+} wts_t;
+
 /* ------------------------------------------------------------------------------------------ */
 /* tanh sum-product, fp32 (bp/bp.py:43-51, bp_vc.py:16-27, bp_cv.py:22-50)                      */
 static int syndrome_ok(const graph_t* g, const uint8_t* bits);
@@ -58,7 +70,7 @@ static int syndrome_ok(const graph_t* g, const uint8_t* bits);
  * z = 0.5*(L + sum x) (bp.py:36-39,51) satisfy every check; returns the iterations run. */
 static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp, float* x, float* v2c,
                       float* p1_out, float* z_out, uint8_t* bits_out, float* trace, int64_t trace_stride,
-                      int early_stop, uint8_t* hb) {
+                      int early_stop, uint8_t* hb, const wts_t* w) {
     const int E = g->E;
     int used = iters;
     for (int e = 0; e < E; ++e) x[e] = 0.0f;
@@ -73,13 +85,15 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
         }
         /* VC + tanh: v2c at check-order ids */
         for (int v = 0; v < g->n; ++v) {
-            const int a = g->var_ptr[v], b = g->var_ptr[v + 1];
+            const int a = g->var_ptr[v], b = g->var_ptr[v + 1], d = b - a;
             const float L = -llr[v];
+            const float* wv = w && w->vn ? (const float*)w->vn + it * w->W + w->wofs[v] : NULL;
+            const float Lw = w && w->lw ? ((const float*)w->lw)[(int64_t)it * g->n + v] * L : L;
             for (int t = a; t < b; ++t) {
                 float S = 0.0f;
                 for (int u = a; u < b; ++u)
-                    if (u != t) S += x[g->var_edges[u]];
-                v2c[g->var_edges[t]] = tanhf(0.5f * (L + S));
+                    if (u != t) S += wv ? wv[(t - a) * d + (u - a)] * x[g->var_edges[u]] : x[g->var_edges[u]];
+                v2c[g->var_edges[t]] = tanhf(0.5f * (Lw + S));
             }
         }
         /* CV */
@@ -101,8 +115,10 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
     }
     for (int v = 0; v < g->n; ++v) {
         float S = 0.0f;
-        for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += x[g->var_edges[u]];
-        const float z = 0.5f * (-llr[v] + S);
+        const float* fw = w && w->fin ? (const float*)w->fin : NULL;
+        for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += fw ? fw[u] * x[g->var_edges[u]] : x[g->var_edges[u]];
+        const float Lf = w && w->flw ? ((const float*)w->flw)[v] * -llr[v] : -llr[v];
+        const float z = 0.5f * (Lf + S);
         if (z_out) z_out[v] = z;
         if (p1_out) p1_out[v] = 1.0f - 1.0f / (1.0f + expf(-z));
         if (bits_out) bits_out[v] = (uint8_t)(z <= ZTHR_F32);
@@ -112,18 +128,20 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
 
 /* tanh sum-product, fp64: the reference module after .double() */
 static void sp_f64_one(const graph_t* g, const double* llr, int iters, double clamp, double* x, double* v2c,
-                       double* p1_out, double* z_out, uint8_t* bits_out) {
+                       double* p1_out, double* z_out, uint8_t* bits_out, const wts_t* w) {
     const int E = g->E;
     for (int e = 0; e < E; ++e) x[e] = 0.0;
     for (int it = 0; it < iters; ++it) {
         for (int v = 0; v < g->n; ++v) {
-            const int a = g->var_ptr[v], b = g->var_ptr[v + 1];
+            const int a = g->var_ptr[v], b = g->var_ptr[v + 1], d = b - a;
             const double L = -llr[v];
+            const double* wv = w && w->vn ? (const double*)w->vn + it * w->W + w->wofs[v] : NULL;
+            const double Lw = w && w->lw ? ((const double*)w->lw)[(int64_t)it * g->n + v] * L : L;
             for (int t = a; t < b; ++t) {
                 double S = 0.0;
                 for (int u = a; u < b; ++u)
-                    if (u != t) S += x[g->var_edges[u]];
-                v2c[g->var_edges[t]] = tanh(0.5 * (L + S));
+                    if (u != t) S += wv ? wv[(t - a) * d + (u - a)] * x[g->var_edges[u]] : x[g->var_edges[u]];
+                v2c[g->var_edges[t]] = tanh(0.5 * (Lw + S));
             }
         }
         for (int c = 0; c < g->m; ++c) {
@@ -143,8 +161,10 @@ static void sp_f64_one(const graph_t* g, const double* llr, int iters, double cl
     }
     for (int v = 0; v < g->n; ++v) {
         double S = 0.0;
-        for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += x[g->var_edges[u]];
-        const double z = 0.5 * (-llr[v] + S);
+        const double* fw = w && w->fin ? (const double*)w->fin : NULL;
+        for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += fw ? fw[u] * x[g->var_edges[u]] : x[g->var_edges[u]];
+        const double Lf = w && w->flw ? ((const double*)w->flw)[v] * -llr[v] : -llr[v];
+        const double z = 0.5 * (Lf + S);
         if (z_out) z_out[v] = z;
         if (p1_out) p1_out[v] = 1.0 - 1.0 / (1.0 + exp(-z));
         if (bits_out) bits_out[v] = (uint8_t)(z < ZTHR_F64);
@@ -272,10 +292,33 @@ static int qms_one(const graph_t* g, const int8_t* qllr, int iters, int qmax, in
 #define GRAPH_ARGS int m, int n, int E, const int32_t *row_ptr, const int32_t *col_idx, \
                    const int32_t *var_ptr, const int32_t *var_edges
 #define MAKE_GRAPH graph_t g = {m, n, E, row_ptr, col_idx, var_ptr, var_edges}
+#define WEIGHT_ARGS const void *w_vn, const void *w_lw, const void *w_fin, const void *w_flw
+
+/* fills wt (and allocates wofs) when any weight array is given; returns the pointer to pass, or NULL */
+static const wts_t* make_wts(const graph_t* g, wts_t* wt, WEIGHT_ARGS) {
+    if (!w_vn && !w_lw && !w_fin && !w_flw) return NULL;
+    int64_t* wofs = (int64_t*)malloc(sizeof(int64_t) * ((size_t)g->n + 1));
+    wofs[0] = 0;
+    for (int v = 0; v < g->n; ++v) {
+        const int64_t d = g->var_ptr[v + 1] - g->var_ptr[v];
+        wofs[v + 1] = wofs[v] + d * d;
+    }
+    wt->vn = w_vn;
+    wt->lw = w_lw;
+    wt->fin = w_fin;
+    wt->flw = w_flw;
+    wt->wofs = wofs;
+    wt->W = wofs[g->n];
+    return wt;
+}
 
 int oracle_sp_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clamp, float* p1, float* z,
-                  uint8_t* bits, float* trace /* [iters][B][E] or NULL */, int early_stop, int32_t* iters_used) {
+                  uint8_t* bits, float* trace /* [iters][B][E] or NULL */, int early_stop, int32_t* iters_used,
+                  WEIGHT_ARGS) {
     MAKE_GRAPH;
+    wts_t wt;
+    const wts_t* w = make_wts(&g, &wt, w_vn, w_lw, w_fin, w_flw);
+    if (w && early_stop) { free((void*)wt.wofs); return -1; }
 #pragma omp parallel
     {
         float* x = (float*)malloc(sizeof(float) * (size_t)E);
@@ -284,19 +327,22 @@ int oracle_sp_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clam
 #pragma omp for schedule(dynamic, 16)
         for (int64_t i = 0; i < B; ++i) {
             int u = sp_f32_one(&g, llr + i * n, iters, clamp, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
-                               bits ? bits + i * n : NULL, trace ? trace + i * E : NULL, B * (int64_t)E, early_stop, hb);
+                               bits ? bits + i * n : NULL, trace ? trace + i * E : NULL, B * (int64_t)E, early_stop, hb, w);
             if (iters_used) iters_used[i] = u;
         }
         free(x);
         free(v2c);
         free(hb);
     }
+    if (w) free((void*)wt.wofs);
     return 0;
 }
 
 int oracle_sp_f64(GRAPH_ARGS, const double* llr, int64_t B, int iters, double clamp, double* p1, double* z,
-                  uint8_t* bits) {
+                  uint8_t* bits, WEIGHT_ARGS) {
     MAKE_GRAPH;
+    wts_t wt;
+    const wts_t* w = make_wts(&g, &wt, w_vn, w_lw, w_fin, w_flw);
 #pragma omp parallel
     {
         double* x = (double*)malloc(sizeof(double) * (size_t)E);
@@ -304,10 +350,11 @@ int oracle_sp_f64(GRAPH_ARGS, const double* llr, int64_t B, int iters, double cl
 #pragma omp for schedule(dynamic, 16)
         for (int64_t i = 0; i < B; ++i)
             sp_f64_one(&g, llr + i * n, iters, clamp, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
-                       bits ? bits + i * n : NULL);
+                       bits ? bits + i * n : NULL, w);
         free(x);
         free(v2c);
     }
+    if (w) free((void*)wt.wofs);
     return 0;
 }
 

@@ -37,8 +37,8 @@ def lib():
         vp = ctypes.c_void_p
         garg = [ctypes.c_int, ctypes.c_int, ctypes.c_int, i32p, i32p, i32p, i32p]
         L.oracle_sp_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, vp, vp, vp, vp,
-                                           ctypes.c_int, vp]
-        L.oracle_sp_f64.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, vp, vp, vp]
+                                           ctypes.c_int, vp] + [vp] * 4
+        L.oracle_sp_f64.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, vp, vp, vp] + [vp] * 4
         L.oracle_ms_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                            ctypes.c_float, ctypes.c_int, vp, vp, vp, vp]
         L.oracle_qms.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -62,9 +62,20 @@ def _gargs(g: Graph):
     return (g.m, g.n, g.E, g.row_ptr, g.col_idx, g.var_ptr, g.var_edges)
 
 
-def sp_f32(H, llr, iters, clamp, trace=False, early_stop=False):
+def _weights(weights, dtype):
+    """weights: None or dict(vn=[iters][W], llr=[iters][n], fin=[E], fin_llr=[n]) in the compact layout of
+    ldpc_oracle.c (any key may be missing = all ones).  Returns the 4 pointers and the arrays to keep alive."""
+    if not weights:
+        return [None] * 4, []
+    arrs = [None if weights.get(k) is None else np.ascontiguousarray(weights[k], dtype=dtype)
+            for k in ("vn", "llr", "fin", "fin_llr")]
+    return [_ptr(a) for a in arrs], arrs
+
+
+def sp_f32(H, llr, iters, clamp, trace=False, early_stop=False, weights=None):
     """tanh sum-product in fp32. Returns dict(p1, z, bits, iters_used[, trace[iters,B,E]])."""
     g = _graph(H)
+    wp, _keep = _weights(weights, np.float32)
     llr = np.ascontiguousarray(llr, dtype=np.float32)
     B = llr.shape[0]
     p1 = np.empty((B, g.n), np.float32)
@@ -73,21 +84,22 @@ def sp_f32(H, llr, iters, clamp, trace=False, early_stop=False):
     tr = np.empty((iters, B, g.E), np.float32) if trace else None
     used = np.empty(B, np.int32)
     lib().oracle_sp_f32(*_gargs(g), _ptr(llr), B, int(iters), float(clamp), _ptr(p1), _ptr(z), _ptr(bits), _ptr(tr),
-                        int(bool(early_stop)), _ptr(used))
+                        int(bool(early_stop)), _ptr(used), *wp)
     out = dict(p1=p1, z=z, bits=bits, iters_used=used)
     if trace:
         out["trace"] = tr
     return out
 
 
-def sp_f64(H, llr, iters, clamp):
+def sp_f64(H, llr, iters, clamp, weights=None):
     g = _graph(H)
+    wp, _keep = _weights(weights, np.float64)
     llr = np.ascontiguousarray(llr, dtype=np.float64)
     B = llr.shape[0]
     p1 = np.empty((B, g.n), np.float64)
     z = np.empty((B, g.n), np.float64)
     bits = np.empty((B, g.n), np.uint8)
-    lib().oracle_sp_f64(*_gargs(g), _ptr(llr), B, int(iters), float(clamp), _ptr(p1), _ptr(z), _ptr(bits))
+    lib().oracle_sp_f64(*_gargs(g), _ptr(llr), B, int(iters), float(clamp), _ptr(p1), _ptr(z), _ptr(bits), *wp)
     return dict(p1=p1, z=z, bits=bits)
 
 

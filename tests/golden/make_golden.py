@@ -19,6 +19,12 @@ What it records (all .npz, numeric arrays only — loadable with allow_pickle=Fa
                            iters 5, clamp 10, Eb/N0 1 and 2 dB, fp32 and fp64.
   * demod_ofdm.npz         ``demodulate_signal`` (``ofdm_functions.py:63-78``) on a fixed received vector:
                            pins the reference's LLR formula/sign convention for the channel front end.
+  * adc_quantizer.npz      ``quantizer`` (``:37-51``) at fixed clips (incl. the lo > hi corner) and
+                           ``gen_qdata`` (``:118-128``, AGC clip = std * ratio) on a complex64-valued stream.
+  * bp_weighted_peg64.npz  weighted BP: the reference module with random per-layer ``input_weight`` /
+                           ``llr_weight`` set in memory (``bp_vc.py:19,24``), 5 iterations, fp32 and fp64.
+
+    python tests/golden/make_golden.py [bp] [adc] [weighted]     (no argument: all)
 """
 import os
 import sys
@@ -73,7 +79,7 @@ def run_ref(H, iters, clamp, llr32, double=False, trace=False):
     return p1.numpy(), (np.stack(snaps) if trace else None)
 
 
-def main():
+def gen_bp():
     H = parity.H.astype(np.int64)
     G = parity.G.astype(np.int64)
     np.savez_compressed(os.path.join(HERE, "peg64_32.npz"), H=H, G=G)
@@ -141,8 +147,67 @@ def main():
     llrs, rsym = OF.demodulate_signal(rx.reshape(1, -1), 32, 10 ** (3.0 / 10))
     np.savez_compressed(os.path.join(HERE, "demod_ofdm.npz"), rx=rx, snr_db=3.0, ofdm_size=32,
                         llrs=llrs, rx_symbols=rsym)
-    print("done")
+
+
+def gen_adc():
+    rng = np.random.default_rng(37)
+    rx = ((rng.standard_normal(4096) + 1j * rng.standard_normal(4096)) * 0.7).astype(np.complex64)
+    rx = rx.astype(np.complex128)  # complex64-representable values, so the fp32 device input is exact
+    rec = dict(rx=rx)
+    fixed = [(1, 0.3), (1, 1.0), (3, 0.8), (5, 2.0), (8, 1.5), (4, 0.45)]
+    for i, (b, c) in enumerate(fixed):
+        rec[f"q_fixed{i}"] = OF.quantizer(rx.reshape(1, -1), b, c).reshape(-1)
+    rec["fixed"] = np.array(fixed, dtype=np.float64)
+    agc = [(3, 1.0), (5, 2.0), (5, 3.0), (8, 1.5)]
+    for i, (b, r) in enumerate(agc):
+        q, qs, ql = OF.gen_qdata(rx.reshape(1, -1), 2.0, b, r, 32)
+        rec[f"q_agc{i}"] = q.reshape(-1)
+        rec[f"qsym_agc{i}"] = qs.reshape(-1)
+        rec[f"qllr_agc{i}"] = ql.reshape(-1)
+        rec[f"clip_agc{i}"] = np.max(np.std(rx.reshape(1, -1))) * r
+    rec["agc"] = np.array(agc, dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "adc_quantizer.npz"), snr_db=2.0, ofdm_size=32, **rec)
+
+
+def gen_weighted():
+    H = parity.H.astype(np.int64)
+    G = parity.G.astype(np.int64)
+    iters, clamp, B = 5, 10.0, 64
+    rng = np.random.default_rng(4242)
+    model = BeliefPropagation(H, iters)
+    rec = {}
+    for i, layer in enumerate(model.layers):
+        vc = layer[0]
+        vc.input_weight.data = vc.mask.data * torch.tensor(rng.uniform(0.5, 1.5, vc.mask.shape), dtype=torch.float)
+        vc.llr_weight.data = torch.tensor(rng.uniform(0.5, 1.5, vc.llr_weight.shape), dtype=torch.float)
+        rec[f"input_weight{i}"] = vc.input_weight.data.numpy().copy()
+        rec[f"llr_weight{i}"] = vc.llr_weight.data.numpy().copy()
+    fv = model.final_layer[0]
+    fv.input_weight.data = fv.mask.data * torch.tensor(rng.uniform(0.5, 1.5, fv.mask.shape), dtype=torch.float)
+    fv.llr_weight.data = torch.tensor(rng.uniform(0.5, 1.5, fv.llr_weight.shape), dtype=torch.float)
+    rec["final_input_weight"] = fv.input_weight.data.numpy().copy()
+    rec["final_llr_weight"] = fv.llr_weight.data.numpy().copy()
+    model.eval()
+    for snr in (1.0, 3.0):
+        info = rng.integers(0, 2, size=(B, 32))
+        cw = (info @ G.T) % 2
+        llr = bpsk_awgn_llr(cw, snr, 0.5, rng)
+        tag = f"snr{int(snr)}"
+        with torch.no_grad():
+            x = torch.zeros(B, model.layer_size())
+            p32 = model(x, torch.tensor(llr), clamp).numpy()
+            m64 = model.double()
+            p64 = m64(x.double(), torch.tensor(llr, dtype=torch.float64), clamp).numpy()
+            model.float()
+        rec[f"llr_{tag}"] = llr
+        rec[f"p1_f32_{tag}"] = p32.astype(np.float32)
+        rec[f"p1_f64_{tag}"] = p64
+        print("weighted", tag, "bit errors:", int((np.round(p32) != cw).sum()))
+    np.savez_compressed(os.path.join(HERE, "bp_weighted_peg64.npz"), H=H, iters=iters, clamp=clamp, **rec)
 
 
 if __name__ == "__main__":
-    main()
+    parts = sys.argv[1:] or ["bp", "adc", "weighted"]
+    for part in parts:
+        {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted}[part]()
+    print("done")

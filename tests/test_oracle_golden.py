@@ -84,3 +84,39 @@ def test_hard_decision_threshold():
     zs = np.array([[thr, thr], [np.nextafter(thr, np.float32(0)), 0.0]], np.float32)
     r = oracle.sp_f32(H, (-2 * zs).astype(np.float32), 0, 10.0)
     assert r["bits"].tolist() == [[1, 1], [0, 0]]
+
+
+def test_weighted_oracle_matches_reference_golden():
+    """Weighted BP (bp_vc.py:19,24 with random non-unit weights set in the reference module): the oracle
+    on the compact weight layout reproduces the reference's fp64 and fp32 p1."""
+    from ldpc_amd.codes import Graph
+    d = np.load(os.path.join(GOLDEN, "bp_weighted_peg64.npz"))
+    H, iters, clamp = d["H"], int(d["iters"]), float(d["clamp"])
+    g = Graph.from_H(H)
+    w = g.compact_weights([d[f"input_weight{i}"] for i in range(iters)], [d[f"llr_weight{i}"] for i in range(iters)],
+                          d["final_input_weight"], d["final_llr_weight"])
+    # every reference weight on the mask is carried over (and nothing off it)
+    tgt, src, pos = g.vn_weight_index()
+    assert np.count_nonzero(d["input_weight0"]) == len(pos)
+    for tag in ("snr1", "snr3"):
+        llr = d[f"llr_{tag}"]
+        r64 = oracle.sp_f64(H, llr.astype(np.float64), iters, clamp, weights=w)
+        assert np.abs(r64["p1"] - d[f"p1_f64_{tag}"]).max() < 1e-12
+        r32 = oracle.sp_f32(H, llr, iters, clamp, weights=w)
+        assert np.abs(r32["p1"] - d[f"p1_f32_{tag}"]).max() < 5e-5
+        assert (r32["bits"] != np.round(d[f"p1_f32_{tag}"])).sum() == 0
+    # all-ones weights reduce to plain BP exactly
+    ones = g.compact_weights([np.ones((g.E, g.E))] * iters, [np.ones((1, g.n))] * iters, np.ones((g.n, g.E)),
+                             np.ones((1, g.n)))
+    llr = d["llr_snr1"]
+    a = oracle.sp_f32(H, llr, iters, clamp, weights=ones)
+    b = oracle.sp_f32(H, llr, iters, clamp)
+    assert np.array_equal(a["z"], b["z"])
+
+
+def test_adc_golden_self_consistent():
+    """The ADC fixture's AGC clip is np.std of the stream times the ratio (gen_qdata :118-124)."""
+    d = np.load(os.path.join(GOLDEN, "adc_quantizer.npz"))
+    rx = d["rx"]
+    for i, (b, r) in enumerate(d["agc"]):
+        assert np.isclose(d[f"clip_agc{i}"], np.std(rx) * r, rtol=1e-15)

@@ -26,20 +26,25 @@ import numpy as np
 from . import _abi
 from .api import get_decoder
 from .codes import get_code
-from .channel import ofdm_demod, ofdm_tx
+from .channel import adc_quantize, ofdm_demod, ofdm_tx
 from .synth import DeviceEncoder
 from .dist import ebn0_sigma, sweep as dist_sweep
 
 
 def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=0.0, snr_db=(0.0,),
         codewords=65536, batch=65536, seed=1, rank=0, world=1, device=0, early_stop=False, qstep=1.0,
-        qmax=15, app_max=127, mod="bpsk", ofdm_size=32):
+        qmax=15, app_max=127, mod="bpsk", ofdm_size=32, adc_bits=None, clip_ratio=2.0):
     """Returns dict(snrdb, uncoded_ber, coded_ber, coded_bler, codewords, seconds).
 
     ``mod``: "bpsk" (BPSK/AWGN LLRs), "qpsk-ofdm" (the reference's chain: modulate_bits, transmit_symbols,
     demodulate_signal), "16qam-ofdm" (16-QAM Gray over OFDM, exact LLRs; not in the reference).  Points
     are Eb/N0 in dB; the OFDM modes transmit at Es/N0 = Eb/N0 * R * bits_per_symbol (R = 1/2 QPSK:
-    Es/N0 = Eb/N0, the reference's "SNR")."""
+    Es/N0 = Eb/N0, the reference's "SNR").
+
+    ``adc_bits`` (OFDM modes only): also run the received samples through the AGC-clipped ADC
+    (``gen_qdata``, ``ofdm_functions.py:118-128``; clip = std(rx of the batch) * ``clip_ratio``) and report
+    evaluate_quantized.py's ``*_quantized`` metrics and ``wmse_quantized`` (``:122``) next to the
+    unquantized ones."""
     import torch
     H, _ = get_code(code) if isinstance(code, str) else (code, None)
     m, n = H.shape
@@ -59,6 +64,11 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
     llr = torch.empty((bmax, n), dtype=torch.float32, device=dev)
     bits = torch.empty((bmax, n), dtype=torch.uint8, device=dev)
     unc = torch.zeros((len(snr_db),), dtype=torch.int64, device=dev)
+    if adc_bits is not None and mod == "bpsk":
+        raise ValueError("adc_bits needs an OFDM modulation (the ADC sees the time-domain samples)")
+    qcnt = torch.zeros((len(snr_db), 3), dtype=torch.int64, device=dev)
+    qunc = torch.zeros((len(snr_db),), dtype=torch.int64, device=dev)
+    wmse = torch.zeros((len(snr_db),), dtype=torch.float64, device=dev)
 
     def run_shard(i, lo, hi, sigma):
         cnt = torch.zeros(3, dtype=torch.int64, device=dev)
@@ -81,28 +91,50 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
             _abi.check(lib.ldpc_decode_ex(dec._h, llr.data_ptr(), B, p, bits.data_ptr(), None, None,
                                           ws.data_ptr(), wsb, st))
             _abi.check(lib.ldpc_count_errors(bits.data_ptr(), cw.data_ptr(), B, n, k, cnt.data_ptr(), st))
+            if adc_bits is not None:
+                ql = ofdm_demod(adc_quantize(rx, adc_bits, clip_ratio=clip_ratio), ofdm_size, bps, esn0)[:B * n].view(B, n)
+                qunc[i] += ((ql > 0).to(torch.uint8) != cw).sum()
+                lv = llr[:B].double()
+                wmse[i] += ((ql.double() - lv) ** 2 / (lv.abs() + 10e-4)).sum()
+                ql = ql.contiguous()
+                _abi.check(lib.ldpc_decode_ex(dec._h, ql.data_ptr(), B, p, bits.data_ptr(), None, None,
+                                              ws.data_ptr(), wsb, st))
+                _abi.check(lib.ldpc_count_errors(bits.data_ptr(), cw.data_ptr(), B, n, k, qcnt[i].data_ptr(), st))
         return cnt.cpu().numpy()
 
     t0 = time.perf_counter()
     res = dist_sweep(list(snr_db), codewords, rate, k, run_shard, rank=rank, world=world, device=dev)
     from .dist import allreduce_counts
-    allreduce_counts(unc)
+    for t in (unc, qcnt, qunc, wmse):
+        allreduce_counts(t)
     secs = time.perf_counter() - t0
     c = res.counts.astype(np.float64)
-    return dict(snrdb=np.asarray(snr_db, dtype=np.float64),
-                uncoded_ber=unc.cpu().numpy() / (c[:, 2] * n),
-                coded_ber=c[:, 0] / (c[:, 2] * k),
-                coded_bler=c[:, 1] / c[:, 2],
-                codewords=c[:, 2].astype(np.int64), seconds=secs,
-                config=dict(code=code if isinstance(code, str) else "custom", algo=algo, iters=iters,
-                            clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop, mod=mod))
+    out = dict(snrdb=np.asarray(snr_db, dtype=np.float64),
+               uncoded_ber=unc.cpu().numpy() / (c[:, 2] * n),
+               coded_ber=c[:, 0] / (c[:, 2] * k),
+               coded_bler=c[:, 1] / c[:, 2],
+               codewords=c[:, 2].astype(np.int64), seconds=secs,
+               config=dict(code=code if isinstance(code, str) else "custom", algo=algo, iters=iters,
+                           clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop, mod=mod,
+                           adc_bits=adc_bits, clip_ratio=clip_ratio if adc_bits is not None else None))
+    if adc_bits is not None:
+        q = qcnt.cpu().numpy().astype(np.float64)
+        out.update(uncoded_ber_quantized=qunc.cpu().numpy() / (c[:, 2] * n),
+                   coded_ber_quantized=q[:, 0] / (c[:, 2] * k), coded_bler_quantized=q[:, 1] / c[:, 2],
+                   wmse_quantized=wmse.cpu().numpy() / (c[:, 2] * n))
+    return out
+
+
+PKL_KEYS = ("snrdb", "uncoded_ber", "coded_ber", "coded_bler", "uncoded_ber_quantized", "coded_ber_quantized",
+            "coded_bler_quantized", "wmse_quantized")
 
 
 def save(result: dict, path: str):
     """``.pkl``: the reference's schema (``evaluate_quantized.py:156-172`` keys snrdb, uncoded_ber,
-    coded_ber, coded_bler as numpy arrays) for plots.py; ``.json``: plain lists."""
+    coded_ber, coded_bler and, with the ADC, the ``*_quantized`` / ``wmse_quantized`` keys, as numpy
+    arrays) for plots.py; ``.json``: plain lists."""
     if path.endswith(".pkl"):
-        keep = {kk: np.asarray(result[kk]) for kk in ("snrdb", "uncoded_ber", "coded_ber", "coded_bler")}
+        keep = {kk: np.asarray(result[kk]) for kk in PKL_KEYS if kk in result}
         with open(path, "wb") as f:
             pickle.dump(keep, f)
     else:
@@ -129,6 +161,8 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--early-stop", action="store_true")
     ap.add_argument("--mod", default="bpsk", choices=["bpsk", "qpsk-ofdm", "16qam-ofdm"])
+    ap.add_argument("--adc-bits", type=int, default=None, help="also decode through the AGC-clipped ADC")
+    ap.add_argument("--clip-ratio", type=float, default=2.0)
     ap.add_argument("--out", default=None, help="results .json or .pkl (reference schema)")
     a = ap.parse_args(argv)
     import torch
@@ -140,11 +174,15 @@ def main(argv=None):
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     r = run(a.code, a.algo, a.iters, a.clamp, a.alpha, a.beta, _parse_points(a.snr), a.n, a.batch, a.seed,
-            rank, world, local, a.early_stop, mod=a.mod)
+            rank, world, local, a.early_stop, mod=a.mod, adc_bits=a.adc_bits, clip_ratio=a.clip_ratio)
     if rank == 0:
         for i, e in enumerate(r["snrdb"]):
-            print(f"{e:5.2f} dB  uncoded {r['uncoded_ber'][i]:.4e}  coded BER {r['coded_ber'][i]:.4e}  "
-                  f"BLER {r['coded_bler'][i]:.4e}  ({r['codewords'][i]} cw)")
+            line = (f"{e:5.2f} dB  uncoded {r['uncoded_ber'][i]:.4e}  coded BER {r['coded_ber'][i]:.4e}  "
+                    f"BLER {r['coded_bler'][i]:.4e}  ({r['codewords'][i]} cw)")
+            if "coded_ber_quantized" in r:
+                line += (f" | ADC uncoded {r['uncoded_ber_quantized'][i]:.4e} BER {r['coded_ber_quantized'][i]:.4e} "
+                         f"BLER {r['coded_bler_quantized'][i]:.4e} wmse {r['wmse_quantized'][i]:.4g}")
+            print(line)
         print(f"{r['seconds']:.2f} s")
         if a.out:
             save(r, a.out)

@@ -62,3 +62,25 @@ def test_16qam_ofdm_sweep_1944_sp():
         nb = 2048 * 1944
         assert abs(r["uncoded_ber"][i] - th) < 5 * np.sqrt(th / nb) + 1e-6, (e, r["uncoded_ber"][i], th)
     assert r["coded_bler"][0] > 0.9 and r["coded_bler"][1] < 0.05, r["coded_bler"]
+
+
+def test_adc_sweep_evaluate_quantized_metrics(tmp_path):
+    """evaluate_quantized.py's quantized leg (gen_qdata -> decode_bits): a fine ADC tracks the unquantized
+    curve, a 2-bit ADC is strictly worse; wmse grows as bits shrink; the .pkl carries the extra keys."""
+    import pickle
+    from ldpc_amd.sweep import save
+    kw = dict(snr_db=[2.0, 4.0], codewords=16384, batch=16384, seed=5, mod="qpsk-ofdm")
+    fine = run("peg64_32", "tanh", 5, 20.0, adc_bits=10, clip_ratio=3.0, **kw)
+    coarse = run("peg64_32", "tanh", 5, 20.0, adc_bits=2, clip_ratio=1.0, **kw)
+    nb = 16384 * 64
+    for i in range(2):
+        u, uq = fine["uncoded_ber"][i], fine["uncoded_ber_quantized"][i]
+        assert abs(u - uq) < 5 * np.sqrt(u / nb) + 2e-4
+        assert coarse["uncoded_ber_quantized"][i] > coarse["uncoded_ber"][i] * 1.05
+        assert 0 < fine["wmse_quantized"][i] < coarse["wmse_quantized"][i]
+    assert np.array_equal(fine["uncoded_ber"], coarse["uncoded_ber"])   # same channel draws
+    p = tmp_path / "q.pkl"
+    save(fine, str(p))
+    with open(p, "rb") as f:
+        d = pickle.load(f)   # our own file
+    assert {"coded_ber_quantized", "coded_bler_quantized", "uncoded_ber_quantized", "wmse_quantized"} <= set(d)

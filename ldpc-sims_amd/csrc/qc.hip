@@ -24,17 +24,11 @@
 
 namespace ldpc {
 
-#ifndef QC_ADDR_SGPR_MASK
-#define QC_ADDR_SGPR_MASK 1  // rotation-address select with a compile-time lane mask (1 VALU, no v_cmp)
-#endif
-#ifndef QC_ID_AT_VN
-#define QC_ID_AT_VN 1  // find the min slot by |v| == min1 at VN time instead of tracking it in CN
-#endif
 #ifndef QC_DIAG_DPP
 #define QC_DIAG_DPP 0
 #endif
-#ifndef QC_ROW_BARRIER
-#define QC_ROW_BARRIER 0  // measured +1.9% without the per-row scheduling barrier
+#ifndef QC_PIPE
+#define QC_PIPE 0  // software-pipelined row order: measured no gain (not latency-bound), kept as an option
 #endif
 #ifndef QC_WAVES_PER_SIMD
 #define QC_WAVES_PER_SIMD 5  // 96 VGPRs: 20 waves (40 codewords at Z=27) resident per CU
@@ -143,22 +137,29 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
     const int zb = (z < Z) ? z : z - Z;
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
-    // invalid lanes read element 0 (B >= 1) and discard it: unconditional loads, no per-load branches
-    const float* lp = llr + (valid ? cw * N + z : 0);
+    // Lane frames (qc_tables.h PHI): lane z holds variable (j, (z + PHI[j]) mod Z); check labels are
+    // rotated too, which is invisible outside.  Circulant (r, j) is then a rotation by SHR[r][t], zero for
+    // a spanning tree's worth of circulants.  A pure relabelling: every value is computed exactly as before.
+    const int64_t cwbase = valid ? cw * N : 0;  // invalid lanes read element 0 (B >= 1) and discard it
     const float vmask = valid ? 1.0f : 0.0f;
+    auto vidx = [&](int zz, int j, int phi) {  // index of this lane's variable of block column j
+        int t = zz + phi;
+        t -= (t >= Z) ? Z : 0;
+        return cwbase + j * Z + (valid ? t : 0);
+    };
     constexpr bool early = EARLY;
 
     // channel LLRs L = -llr (quantized in QUANT mode) staged once in LDS: [wave][half][j][z]
     __shared__ float Ls[4 * CPW * N];
     const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
     float app[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-        float x = lp[j * Z] * vmask;
+    static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        float x = llr[vidx(z, j, C::PHI[j])] * vmask;
         if (QUANT) x = fminf(fmaxf(rintf(x * qinv), -qmax), qmax);
         app[j] = -x;  // APP before iteration 0 = L + sum(c2v = 0)
         if (z < Z) Ls[lbase + j * Z] = app[j];
-    }
+    });
     if (QUANT) {
 #pragma unroll
         for (int j = 0; j < NB; ++j) app[j] = fminf(fmaxf(app[j], -app_max), app_max);
@@ -182,29 +183,38 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
     for (int it = 0; it < iters && running; ++it) {
         float nap[NB];  // APP_{it+1} = L + sum of new c2v; L_j is read from LDS in the first row touching j
         uint64_t unsat = 0;  // checks (lanes) whose parity over APP_it is odd
-        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+        // gather: APP_it of row r's variables rotated into the check frame
+        auto gather = [&](auto rr, float* g) __attribute__((always_inline)) {
             constexpr int r = decltype(rr)::value;
-            constexpr int d = C::DEG[r];
-            // Row boundary: fresh (opaque) lane constants stop GVN/LICM from keeping equal-shift rotation
-            // addresses of different rows (and iterations) alive; the scheduling barrier keeps those
-            // copies inside their row instead of at the loop head.
-#if QC_ROW_BARRIER
-            __builtin_amdgcn_sched_barrier(0);
-#endif
-#if QC_ADDR_SGPR_MASK
-            // the volatile sel_lanes asm already keeps addresses per row; only the LDS base of the L
-            // reloads must be opaque (else LICM hoists the loop-invariant LDS loads: +24 VGPRs)
-            const int br = base4, bmr = base4m;
+            static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int j = C::COL[r][t], s = C::SHR[r][t];
+                if constexpr (s == 0) {
+                    g[t] = app[j];
+                } else {
+                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(base4, base4m) + 4 * s;
+                    g[t] = bperm(addr, app[j]);
+                }
+            });
+        };
+        // add row r's c2v (already rotated back to the variable frame) into APP_{it+1}, ascending rows
+        auto accumulate = [&](auto rr, const float* cr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            // opaque LDS base: else LICM hoists the loop-invariant L reloads out of the loop (+24 VGPRs)
             int lr = lbase;
             asm volatile("" : "+v"(lr));
-#else
-            int zr = z, br = base4, bmr = base4m, lr = lbase;
-            asm volatile("" : "+v"(zr), "+v"(br), "+v"(bmr), "+v"(lr));
-#endif
-            static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-                constexpr int j = decltype(jj)::value;
+            static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int j = C::COL[r][t];
                 if constexpr (first_row<C>(j) == r) nap[j] = Ls[lr + j * Z];
+                nap[j] = nap[j] + cr[t];
             });
+        };
+        // check-node update of row r from its gathered APPs g: new compressed state, outgoing c2v
+        // messages rotated to the variable frame into cr (the rotation is issued, not waited for)
+        auto check_row = [&](auto rr, const float* g, float* cr, auto&& between) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            constexpr int d = C::DEG[r];
             const uint32_t idx_old = pk[r] >> 27;
             float v[d];
             float mn1 = __builtin_inff(), mn2 = __builtin_inff();
@@ -212,18 +222,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
             uint32_t par = 0;  // bit 31 = parity of the hard decisions of this check's variables
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
-                constexpr int j = C::COL[r][t], s = C::SH[r][t];
-                float a;
-                if constexpr (s == 0) {
-                    a = app[j];
-                } else {
-#if QC_ADDR_SGPR_MASK
-                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(br, bmr) + 4 * s;
-#else
-                    const int addr = ((zr >= Z - s) ? bmr : br) + 4 * s;
-#endif
-                    a = bperm(addr, app[j]);
-                }
+                const float a = g[t];
                 // hard bit(APP) = APP <= thr2 <=> APP - thr2n < 0, thr2n = next float above thr2: a
                 // difference of distinct floats is never 0 and never changes sign (denormals kept)
                 if constexpr (early) par ^= __float_as_uint(a - thr2n);
@@ -233,49 +232,64 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
                 if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
                 v[t] = x;
                 const float m = fabsf(x);
-#if !QC_ID_AT_VN
-                id = (m < mn1) ? (uint32_t)t : id;
-#endif
                 mn2 = __builtin_amdgcn_fmed3f(mn1, m, mn2);
                 mn1 = fminf(mn1, m);
                 tot ^= __float_as_uint(x);
             });
             if constexpr (early) unsat |= __ballot((int)par < 0);
+            between();  // pipelined order: next row's gathers / previous row's adds go here
             tot &= 0x80000000u;
             const float M1 = mag_of<NORM>(mn1, alpha, beta, clamp);
             const float M2 = mag_of<NORM>(mn2, alpha, beta, clamp);
             uint32_t sg = 0;
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
-                constexpr int j = C::COL[r][t], s = C::SH[r][t];
-#if QC_ID_AT_VN
+                constexpr int s = C::SHR[r][t];
                 // the min slot is the one with |v| == min1; if several tie, min2 == min1 and M2 == M1,
                 // so the choice (and the stored argmin) cannot change any value: bit-exact vs the oracle
                 const bool ismin = fabsf(v[t]) == mn1;
                 const float mg = ismin ? M2 : M1;
                 id = ismin ? (uint32_t)t : id;
-#else
-                const float mg = (id == (uint32_t)t) ? M2 : M1;
-#endif
                 const float c = __uint_as_float(__float_as_uint(mg) | ((tot ^ __float_as_uint(v[t])) & 0x80000000u));
                 sg = __builtin_amdgcn_alignbit(sg, __float_as_uint(c), 31);
-                float cr;
                 if constexpr (s == 0) {
-                    cr = c;
+                    cr[t] = c;
                 } else {
-#if QC_ADDR_SGPR_MASK
-                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(br, bmr) + 4 * (Z - s);
-#else
-                    const int addr = ((zr >= s) ? bmr : br) + 4 * (Z - s);
-#endif
-                    cr = bperm(addr, c);
+                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
+                    cr[t] = bperm(addr, c);
                 }
-                nap[j] = nap[j] + cr;
             });
+            asm("" : "+v"(id));  // keep the argmin a small integer (else the shift folds into per-slot constants)
             mag1[r] = M1;
             mag2[r] = M2;
             pk[r] = sg | (id << 27);
+        };
+#if QC_PIPE
+        // software-pipelined rows: row r+1's gathers are issued and row r-1's rotated c2v are added while
+        // row r computes, so no row waits on its own LDS round trips.  Per column the adds stay in
+        // ascending row order: bit-exact.
+        float gA[C::MAXDC], gB[C::MAXDC], cA[C::MAXDC], cB[C::MAXDC];
+        gather(std::integral_constant<int, 0>{}, gA);
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            float* gcur = (r & 1) ? gB : gA;
+            float* gnxt = (r & 1) ? gA : gB;
+            float* ccur = (r & 1) ? cB : cA;
+            float* cprv = (r & 1) ? cA : cB;
+            check_row(rr, gcur, ccur, [&]() __attribute__((always_inline)) {
+                if constexpr (r + 1 < MB) gather(std::integral_constant<int, r + 1>{}, gnxt);
+                if constexpr (r >= 1) accumulate(std::integral_constant<int, r - 1>{}, cprv);
+            });
         });
+        accumulate(std::integral_constant<int, MB - 1>{}, ((MB - 1) & 1) ? cB : cA);
+#else
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            float g[C::MAXDC], c[C::MAXDC];
+            gather(rr, g);
+            check_row(rr, g, c, []() {});
+            accumulate(rr, c);
+        });
+#endif
         if constexpr (early) {
             // APP_{it} (this iteration's input) satisfied every check of this codeword: freeze it; the
             // lanes keep running for the wave's other codeword, and their nap is discarded.
@@ -294,15 +308,165 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
         }
     }
     if (valid) {
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
+        int zo = z;  // opaque: the store indices must not be CSE'd with the load indices (48 VGPRs live)
+        asm volatile("" : "+v"(zo));
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            const int64_t o = vidx(zo, j, C::PHI[j]);
             const float zz = 0.5f * app[j];
-            if (bits) bits[cw * N + j * Z + z] = (uint8_t)(zz <= kZthrF32);
-            if (soft) soft[cw * N + j * Z + z] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + expf(-zz));
-        }
+            if (bits) bits[o] = (uint8_t)(zz <= kZthrF32);
+            if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + expf(-zz));
+        });
     }
     if (valid && z == 0 && iters_used) iters_used[cw] = used;
 }
+
+// Stored-message variant (fixed iteration count): every edge's c2v message is kept in a VGPR in the
+// VARIABLE frame, so the check update needs no reconstruction from a compressed state and the variable
+// update no re-compression.  Per iteration: v2c = APP - c2v in place for all edges (APP is then dead),
+// then per row: gather v2c into the check frame, two-minimum + sign product, scatter the new c2v back
+// (in place) and add it into APP_{it+1} in ascending row order.  Same arithmetic as k_qc_ms / the
+// oracle, operation for operation.  The register kernel is instruction-fetch bound (SQC_ICACHE_BUSY ~
+// 100%): this form executes ~12 instead of ~17 instructions (~76 instead of ~124 bytes) per edge, at
+// <= 128 VGPRs (4 waves per SIMD).
+template <class C>
+constexpr int edge_off(int r) {
+    int o = 0;
+    for (int q = 0; q < r; ++q) o += C::DEG[q];
+    return o;
+}
+
+#ifndef QC_ST_WAVES_PER_SIMD
+#define QC_ST_WAVES_PER_SIMD 4  // 128 VGPRs; measured 30.6M cw/s vs 26.2M at 3 waves (648, 50 it)
+#endif
+
+template <class C, bool QUANT, int NORM>
+__global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const float* __restrict__ llr, int64_t B, int iters,
+                                                                       float clamp, float alpha, float beta, float qmax,
+                                                                       float app_max, float qinv, int flags,
+                                                                       uint8_t* __restrict__ bits, float* __restrict__ soft) {
+    constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
+    constexpr int NE = edge_off<C>(MB);
+    static_assert(Z <= 64, "register kernel needs Z <= 64");
+    constexpr int CPW = (Z <= 32) ? 2 : 1;
+    const int lane = threadIdx.x & 63;
+    const int half = (CPW == 2) ? (lane >> 5) : 0;
+    const int z = (CPW == 2) ? (lane & 31) : lane;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t cw = wave * CPW + half;
+    const bool valid = (z < Z) && (cw < B);
+    const int zb = (z < Z) ? z : z - Z;
+    const int base4 = (half * 32 + zb) * 4;
+    const int base4m = base4 - 4 * Z;
+    const int64_t cwbase = valid ? cw * N : 0;
+    const float vmask = valid ? 1.0f : 0.0f;
+    auto vidx = [&](int zz, int j, int phi) {
+        int t = zz + phi;
+        t -= (t >= Z) ? Z : 0;
+        return cwbase + j * Z + (valid ? t : 0);
+    };
+    __shared__ float Ls[4 * CPW * N];
+    const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
+    float app[NB];
+    static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        float x = llr[vidx(z, j, C::PHI[j])] * vmask;
+        if (QUANT) x = fminf(fmaxf(rintf(x * qinv), -qmax), qmax);
+        app[j] = -x;
+        if (z < Z) Ls[lbase + j * Z] = app[j];
+    });
+    if (QUANT) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) app[j] = fminf(fmaxf(app[j], -app_max), app_max);
+    }
+    float msg[NE];  // c2v of every edge (variable frame); v2c in place during an iteration
+#pragma unroll
+    for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
+
+    for (int it = 0; it < iters; ++it) {
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int e = edge_off<C>(r) + t;
+                float x = app[C::COL[r][t]] - msg[e];
+                if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
+                msg[e] = x;
+            });
+        });
+        float nap[NB];
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            constexpr int d = C::DEG[r];
+            constexpr int e0 = edge_off<C>(r);
+            float v[d];
+            float mn1 = __builtin_inff(), mn2 = __builtin_inff();
+            uint32_t tot = 0;
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int s = C::SHR[r][t];
+                float x;
+                if constexpr (s == 0) {
+                    x = msg[e0 + t];
+                } else {
+                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(base4, base4m) + 4 * s;
+                    x = bperm(addr, msg[e0 + t]);
+                }
+                v[t] = x;
+                const float m = fabsf(x);
+                mn2 = __builtin_amdgcn_fmed3f(mn1, m, mn2);
+                mn1 = fminf(mn1, m);
+                tot ^= __float_as_uint(x);
+            });
+            tot &= 0x80000000u;
+            // sign of the product folded into the two magnitudes once per row
+            const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);
+            const float M2 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn2, alpha, beta, clamp)) ^ tot);
+            int lr = lbase;
+            asm volatile("" : "+v"(lr));
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int j = C::COL[r][t], s = C::SHR[r][t];
+                // |v| == min1 picks the min slot; ties imply min2 == min1 (bit-exact, see k_qc_ms)
+                const float mg = (fabsf(v[t]) == mn1) ? M2 : M1;
+                const float c = __uint_as_float(__float_as_uint(mg) ^ (__float_as_uint(v[t]) & 0x80000000u));
+                float cr;
+                if constexpr (s == 0) {
+                    cr = c;
+                } else {
+                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
+                    cr = bperm(addr, c);
+                }
+                msg[e0 + t] = cr;
+                if constexpr (first_row<C>(j) == r) nap[j] = Ls[lr + j * Z];
+                nap[j] = nap[j] + cr;
+            });
+        });
+#pragma unroll
+        for (int j = 0; j < NB; ++j) app[j] = QUANT ? fminf(fmaxf(nap[j], -app_max), app_max) : nap[j];
+    }
+    // epilogue indices recomputed from the thread id (opaque), so nothing but the loop state is live
+    // across the loop (the 4-waves/SIMD register budget is 128)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int zo = (CPW == 2) ? (tid & 31) : (tid & 63);
+    const int64_t cwo = (((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0);
+    if (zo < Z && cwo < B) {
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            int t = zo + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            const int64_t o = cwo * N + j * Z + t;
+            const float zz = 0.5f * app[j];
+            if (bits) bits[o] = (uint8_t)(zz <= kZthrF32);
+            if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + expf(-zz));
+        });
+    }
+}
+
+#ifndef QC_STORED
+#define QC_STORED 1  // fixed-iteration launches use k_qc_ms_st
+#endif
 
 template <class C>
 static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
@@ -315,13 +479,25 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     float* sf = (float*)soft;
     if (p.algo == LDPC_ALGO_QMIN_SUM) {
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
-#define QL(E, N) k_qc_ms<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used)
+#define QL(E, N)                                                                                                  \
+    do {                                                                                                          \
+        if (QC_STORED && !E)                                                                                      \
+            k_qc_ms_st<C, true, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf); \
+        else                                                                                                      \
+            k_qc_ms<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
+    } while (0)
         if (b != 0.0f) { if (es) QL(true, NORM_BETA); else QL(false, NORM_BETA); }
         else           { if (es) QL(true, NORM_PLAIN); else QL(false, NORM_PLAIN); }
 #undef QL
     } else {
         const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
-#define FL(E, N) k_qc_ms<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used)
+#define FL(E, N)                                                                                                  \
+    do {                                                                                                          \
+        if (QC_STORED && !E)                                                                                      \
+            k_qc_ms_st<C, false, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf); \
+        else                                                                                                      \
+            k_qc_ms<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
+    } while (0)
 #define FL2(N) do { if (es) FL(true, N); else FL(false, N); } while (0)
         switch (norm) {
             case NORM_PLAIN: FL2(NORM_PLAIN); break;
@@ -332,6 +508,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #undef FL2
 #undef FL
     }
+    if (QC_STORED && !es && used) fill_i32(used, B, p.iters, st);  // fixed iteration count
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
     return LDPC_OK;

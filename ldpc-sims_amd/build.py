@@ -1,7 +1,11 @@
-"""Build libldpc_hip.so in-tree for gfx950 (hipcc cross-compiles; no GPU needed)."""
+"""Build libldpc_hip.so in-tree for gfx950 (hipcc cross-compiles; no GPU needed).
+
+Each source compiles to its own object (in parallel), then one link; per-file flags below.
+"""
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -11,20 +15,39 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off",  # min-sum must round exactly like oracle/ldpc_oracle.c (no FMA contraction)
          "-fno-slp-vectorize",  # v_pk_* f32 pairs need aligned register pairs: +100 VGPRs in the QC kernel
          "-Wall", "-Wno-unused-function"]
+# The QC register kernels compute on finite values only (min/max of |messages|, no NaN can arise from
+# finite LLRs): without IEEE-mode NaN semantics hipcc drops the canonicalising v_max before each v_min
+# and the min(+inf, x) of the first slot: -5 % instructions in an instruction-fetch-bound loop.  The
+# results for finite inputs are identical (only NaN quieting differs).
+PER_FILE = {"qc.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
 
 
-def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), per_file=True) -> str:
     srcs = [os.path.join(HERE, "csrc", s) for s in SRCS]
     deps = srcs + [os.path.join(HERE, "csrc", "common.h"), os.path.join(ROOT, "include", "ldpc_abi.h")]
     deps += [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
     deps.append(os.path.abspath(__file__))
     if not force and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
-    cmd = ["hipcc", *FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"),
-           "-I", os.path.join(HERE, "csrc"), "-o", out, *srcs]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd)
+    objdir = os.path.join(os.path.dirname(os.path.abspath(out)), "." + os.path.basename(out) + ".objs")
+    os.makedirs(objdir, exist_ok=True)
+    common = ["hipcc", *[f for f in FLAGS if f != "-shared"], *[f"-D{d}" for d in defines],
+              "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")]
+    objs, cmds = [], []
+    for src in srcs:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        cmds.append([*common, *(PER_FILE.get(os.path.basename(src), []) if per_file else []), "-c", "-o", obj, src])
+    link = ["hipcc", "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out, *objs]
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+
+    with ThreadPoolExecutor(max_workers=len(cmds)) as ex:
+        list(ex.map(run, cmds))
+    run(link)
     return out
 
 
@@ -33,4 +56,5 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     out = args[args.index("--out") + 1] if "--out" in args else OUT
     defs = [a[2:] for a in args if a.startswith("-D")]
-    print(build(force="--force" in args or bool(defs), verbose=True, out=out, defines=defs))
+    print(build(force="--force" in args or bool(defs) or "--no-per-file" in args, verbose=True, out=out,
+                defines=defs, per_file="--no-per-file" not in args))

@@ -9,6 +9,10 @@ data-path exchange, so scaling is weak).
 
     python bench.py [--gpus N --steps K --warmup W]                  # N=1
     torchrun --nproc-per-node N ... bench.py --gpus N ...            # one rank per GPU
+
+The other BASELINE.json configs are parity-test cases; their throughput lines (profiles/) come from
+the same script, e.g. configs[2]: --code wifi1944_56 --algo tanh --mod 16qam-ofdm --ebn0 4:0.5:9;
+configs[3]: --code wifi1296_23 --algo qminsum --iters 20 --early-stop; configs[4]: --code dvbs2s_12.
 """
 import argparse
 import json
@@ -46,6 +50,10 @@ def main():
     ap.add_argument("--ebn0", default="0:0.5:5")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--force-generic", action="store_true")
+    ap.add_argument("--early-stop", action="store_true", help="syndrome early termination (cw/s then depends on Eb/N0)")
+    ap.add_argument("--qstep", type=float, default=1.0, help="qminsum: LLR quantisation step (5-bit: qmax 15)")
+    ap.add_argument("--mod", default="bpsk", choices=["bpsk", "qpsk-ofdm", "16qam-ofdm"],
+                    help="LLR generator (outside the timed region): BPSK/AWGN or the OFDM front end")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -91,12 +99,23 @@ def main():
     cw = enc.encode(info)
     llrs = []
     for i, e in enumerate(ebn0):
-        sigma = float(np.sqrt(1.0 / (2.0 * rate * 10.0 ** (e / 10.0))))
         x = torch.empty((B, n), dtype=torch.float32, device="cuda")
-        _abi.check(lib.ldpc_awgn_llr(cw.data_ptr(), x.data_ptr(), B, n, sigma, args.seed * 1000 + i, rank * B, st))
+        if args.mod == "bpsk":
+            sigma = float(np.sqrt(1.0 / (2.0 * rate * 10.0 ** (e / 10.0))))
+            _abi.check(lib.ldpc_awgn_llr(cw.data_ptr(), x.data_ptr(), B, n, sigma, args.seed * 1000 + i, rank * B, st))
+        else:
+            from ldpc_amd.channel import ofdm_demod, ofdm_tx
+            bps = 2 if args.mod == "qpsk-ofdm" else 4
+            esn0 = float(10.0 ** (e / 10.0) * rate * bps)
+            s_ = cw.view(-1)
+            pad = (-s_.numel()) % (bps * 32)
+            if pad:
+                s_ = torch.cat([s_, torch.zeros(pad, dtype=torch.uint8, device="cuda")])
+            rx = ofdm_tx(s_, 32, bps, esn0, args.seed * 1000 + i, rank * B * n // bps)
+            x.copy_(ofdm_demod(rx, 32, bps, esn0)[:B * n].view(B, n))
         llrs.append(x)
-    p = dec.params(args.iters, args.algo, args.clamp, args.alpha, 0.0, False, "f32", "p1",
-                   force_generic=args.force_generic, device_ptrs=True)
+    p = dec.params(args.iters, args.algo, args.clamp, args.alpha, 0.0, args.early_stop, "f32", "p1",
+                   qstep=args.qstep, force_generic=args.force_generic, device_ptrs=True)
     wsb = dec.workspace_bytes(B, p)
     ws = torch.empty((wsb,), dtype=torch.uint8, device="cuda")
     bits = torch.empty((B, n), dtype=torch.uint8, device="cuda")
@@ -140,7 +159,8 @@ def main():
 
     # ---- roofline: algorithmic bytes per decode launch / event-timed launch duration ----
     E = int(H.sum())  # nnz (SparseCode.sum() too)
-    bpc = algorithmic_bytes_per_cw(n, E, args.iters)
+    s_b = 1 if args.algo in ("qminsum", "qms") else 4  # 5-bit mode s_m = s_L = 1 byte
+    bpc = algorithmic_bytes_per_cw(n, E, args.iters, s_b, s_b)
     achieved = bpc * B / (gpu_ms * 1e-3) / 1e9
     peak = 8000.0
     traffic = None
@@ -170,12 +190,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: random info bits, systematic 802.11n encoder, BPSK/AWGN LLRs generated on device",
+            "data": f"synthetic: random info bits, systematic encoder, {args.mod} LLRs generated on device",
             "config": {
-                "workload": f"{args.code} {args.algo} {args.iters} iters, B={B} codewords/GPU/step, "
-                            f"Eb/N0 {args.ebn0} dB cycled per step",
+                "workload": f"{args.code} {args.algo} {args.iters} iters{' early-stop' if args.early_stop else ''}, "
+                            f"B={B} codewords/GPU/step, Eb/N0 {args.ebn0} dB cycled per step",
                 "code": args.code, "n": n, "k": k, "edges": E, "algo": args.algo, "iters": args.iters,
-                "clamp": args.clamp, "alpha": args.alpha, "batch_per_gpu": B, "global_batch": B * world,
+                "clamp": args.clamp, "alpha": args.alpha, "early_stop": args.early_stop, "mod": args.mod,
+                "batch_per_gpu": B, "global_batch": B * world,
                 "parallelism": f"dp{world} (codeword shards, RCCL all-reduce of error counts only)",
                 "kernel_path": "generic-csr" if (args.force_generic or not dec.qc_z) else f"qc-z{dec.qc_z}",
             },
@@ -208,9 +229,12 @@ def cpu_baseline(H, args, rate):
     def run(x):
         t = time.perf_counter()
         if args.algo in ("minsum", "ms", "min_sum"):
-            oracle.ms_f32(H, x, args.iters, args.clamp, args.alpha, 0.0)
+            oracle.ms_f32(H, x, args.iters, args.clamp, args.alpha, 0.0, early_stop=args.early_stop)
+        elif args.algo in ("qminsum", "qms"):
+            q = np.clip(np.rint(x / args.qstep), -15, 15).astype(np.int8)
+            oracle.qms(H, q, args.iters, early_stop=args.early_stop)
         else:
-            oracle.sp_f32(H, x, args.iters, args.clamp)
+            oracle.sp_f32(H, x, args.iters, args.clamp, early_stop=args.early_stop)
         return time.perf_counter() - t
 
     threads = oracle.num_threads()
@@ -219,7 +243,8 @@ def cpu_baseline(H, args, rate):
     Bs = int(min(1 << 17, max(cal, cal * args.cpu_seconds / max(tc, 1e-6))))
     t = run(sample(Bs))
     return {"value": Bs / t, "unit": "codewords/s", "cores": threads, "kind": "port",
-            "sample": f"{Bs} codewords of {args.code} {args.algo} {args.iters} iters at Eb/N0 2.5 dB "
+            "sample": f"{Bs} codewords of {args.code} {args.algo} {args.iters} iters"
+                      f"{' early-stop' if args.early_stop else ''} at Eb/N0 2.5 dB "
                       f"({t:.1f} s, oracle/ldpc_oracle.c, OpenMP {threads} threads)"}
 
 

@@ -464,6 +464,149 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
     }
 }
 
+// ---- tanh sum-product, register-resident (the reference's algorithm on-chip) ---------------------
+// Messages in the variable frame, one VGPR per edge (c2v between iterations, v2c inside one).  The
+// operation order is the oracle's and the generic kernels' (bp_vc.py:16-27, bp_cv.py:22-50): per
+// variable, v2c_t = tanh(0.5 * (L + S_t)) with S_t the ascending sum skipping t, formed prefix-then-
+// continue; per check, p_t = the ascending product skipping t, clamped to +-(1-1e-7), then
+// log((1+p)/(1-p)) clamped to +-clamp; final z = 0.5 * (L + ascending sum).  Same tanhf/logf/expf, so the
+// values equal the generic GPU path's.
+template <class C>
+constexpr int col_deg(int j) {
+    int d = 0;
+    for (int r = 0; r < C::MB; ++r)
+        for (int t = 0; t < C::DEG[r]; ++t) d += (C::COL[r][t] == j);
+    return d;
+}
+template <class C>
+constexpr int col_edge(int j, int k) {  // k-th edge of block column j in ascending row order
+    int c = 0;
+    for (int r = 0; r < C::MB; ++r)
+        for (int t = 0; t < C::DEG[r]; ++t)
+            if (C::COL[r][t] == j) {
+                if (c == k) return edge_off<C>(r) + t;
+                ++c;
+            }
+    return -1;
+}
+
+#ifndef QC_SP_WAVES_PER_SIMD
+#define QC_SP_WAVES_PER_SIMD 4
+#endif
+
+template <class C>
+__global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const float* __restrict__ llr, int64_t B, int iters,
+                                                                       float clamp, int flags, uint8_t* __restrict__ bits,
+                                                                       float* __restrict__ soft) {
+    constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
+    constexpr int NE = edge_off<C>(MB);
+    static_assert(Z <= 64, "register kernel needs Z <= 64");
+    constexpr int CPW = (Z <= 32) ? 2 : 1;
+    const int lane = threadIdx.x & 63;
+    const int half = (CPW == 2) ? (lane >> 5) : 0;
+    const int z = (CPW == 2) ? (lane & 31) : lane;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t cw = wave * CPW + half;
+    const bool valid = (z < Z) && (cw < B);
+    const int zb = (z < Z) ? z : z - Z;
+    const int base4 = (half * 32 + zb) * 4;
+    const int base4m = base4 - 4 * Z;
+    __shared__ float Ls[4 * CPW * N];
+    const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
+    {
+        const int64_t cwbase = valid ? cw * N : 0;
+        const float vmask = valid ? 1.0f : 0.0f;
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            int t = z + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            const float x = llr[cwbase + j * Z + (valid ? t : 0)] * vmask;
+            if (z < Z) Ls[lbase + j * Z] = -x;  // L = -llr (bp.py:47)
+        });
+    }
+    float msg[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
+    const float pmax = kPmaxF32;
+
+    for (int it = 0; it < iters; ++it) {
+        // VC + tanh in the variable frame: c2v -> v2c in place
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            constexpr int dj = col_deg<C>(j);
+            int lr = lbase;
+            asm volatile("" : "+v"(lr));
+            const float L = Ls[lr + j * Z];
+            float P = 0.0f;
+            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
+                constexpr int k = decltype(kk)::value;
+                constexpr int e = col_edge<C>(j, k);
+                float S = P;
+                static_for<k + 1, dj>([&](auto uu) __attribute__((always_inline)) {
+                    S += msg[col_edge<C>(j, decltype(uu)::value)];
+                });
+                const float v = Num<float>::tanh_(0.5f * (L + S));
+                P += msg[e];
+                msg[e] = v;
+            });
+        });
+        // CV in the check frame: gather v2c, exclusive products, log, clamp, scatter c2v back
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            constexpr int d = C::DEG[r];
+            constexpr int e0 = edge_off<C>(r);
+            float g[d];
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int s = C::SHR[r][t];
+                if constexpr (s == 0) {
+                    g[t] = msg[e0 + t];
+                } else {
+                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(base4, base4m) + 4 * s;
+                    g[t] = bperm(addr, msg[e0 + t]);
+                }
+            });
+            float Q = 1.0f;
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int s = C::SHR[r][t];
+                float p = Q;
+                static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
+                Q *= g[t];
+                if (p > pmax) p = pmax;
+                if (p < -pmax) p = -pmax;
+                float y = Num<float>::log_((1.0f + p) / (1.0f - p));
+                if (y > clamp) y = clamp;
+                if (y < -clamp) y = -clamp;
+                if constexpr (s == 0) {
+                    msg[e0 + t] = y;
+                } else {
+                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
+                    msg[e0 + t] = bperm(addr, y);
+                }
+            });
+        });
+    }
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int zo = (CPW == 2) ? (tid & 31) : (tid & 63);
+    const int64_t cwo = (((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0);
+    if (zo < Z && cwo < B) {
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            constexpr int dj = col_deg<C>(j);
+            float S = 0.0f;
+            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) { S += msg[col_edge<C>(j, decltype(kk)::value)]; });
+            const float zz = 0.5f * (Ls[lbase + j * Z] + S);
+            int t = zo + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            const int64_t o = cwo * N + j * Z + t;
+            if (bits) bits[o] = (uint8_t)Num<float>::bit(zz);
+            if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
+        });
+    }
+}
+
 #ifndef QC_STORED
 #define QC_STORED 1  // fixed-iteration launches use k_qc_ms_st
 #endif
@@ -477,7 +620,10 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
     const float* x = (const float*)llr;
     float* sf = (float*)soft;
-    if (p.algo == LDPC_ALGO_QMIN_SUM) {
+    if (p.algo == LDPC_ALGO_TANH_SP) {  // qc_supports: fixed iteration count only
+        k_qc_sp_st<C><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf);
+        if (used) fill_i32(used, B, p.iters, st);
+    } else if (p.algo == LDPC_ALGO_QMIN_SUM) {
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
 #define QL(E, N)                                                                                                  \
     do {                                                                                                          \
@@ -508,7 +654,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #undef FL2
 #undef FL
     }
-    if (QC_STORED && !es && used) fill_i32(used, B, p.iters, st);  // fixed iteration count
+    if (QC_STORED && !es && used && p.algo != LDPC_ALGO_TANH_SP) fill_i32(used, B, p.iters, st);  // fixed count
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
     return LDPC_OK;
@@ -540,6 +686,7 @@ int qc_z(const QCSpec* s) { return s ? s->z : 0; }
 bool qc_supports(const QCSpec* s, const ldpc_params& p) {
     if (!s) return false;
     if (p.flags & LDPC_F_F64) return false;
+    if (p.algo == LDPC_ALGO_TANH_SP) return !(p.flags & LDPC_F_EARLY_STOP);  // on-chip tanh-SP: fixed iterations
     return p.algo == LDPC_ALGO_MIN_SUM || p.algo == LDPC_ALGO_QMIN_SUM;
 }
 

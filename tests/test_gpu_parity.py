@@ -260,3 +260,25 @@ def test_generic_early_stop_vs_oracle(code, algo):
     assert np.array_equal(r["iters_used"], ref["iters_used"])
     assert np.array_equal(r["bits"], ref["bits"])
     assert (ref["iters_used"] < 20).any()          # the test exercises convergence
+
+
+@pytest.mark.parametrize("code", QC_CODES)
+@pytest.mark.parametrize("B", [1, 1001])
+def test_qc_sp_equals_generic_sp_bitwise(code, B):
+    """The on-chip tanh-SP kernel performs the generic kernels' operations in the same order with the
+    same tanhf/logf, so z (and p1) agree bit for bit; both match the oracle's hard bits."""
+    H, qc = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, B, 1.5 if rate < 0.6 else 3.0, seed=21, rate=rate)
+    llr[0, ::5] = 0.0
+    if B > 2:
+        llr[1] = np.float32(60.0)
+    dec = ldpc_amd.get_decoder(H)
+    x = torch.from_numpy(llr).cuda()
+    for soft in ("z", "p1"):
+        a = dec.decode(x, 30, algo="tanh", clamp=10.0, soft=soft)
+        b = dec.decode(x, 30, algo="tanh", clamp=10.0, soft=soft, force_generic=True)
+        assert torch.equal(a["bits"], b["bits"])
+        assert torch.equal(a["soft"].view(torch.int32), b["soft"].view(torch.int32))
+    r = dec.decode(x, 30, algo="tanh", clamp=10.0, want_iters=True)
+    assert bool((r["iters_used"] == 30).all())

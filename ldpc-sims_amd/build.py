@@ -16,19 +16,22 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-fno-slp-vectorize",  # v_pk_* f32 pairs need aligned register pairs: +100 VGPRs in the QC kernel
          "-Wall", "-Wno-unused-function"]
 # The QC register kernels compute on finite values only (min/max of |messages|, no NaN can arise from
-# finite LLRs): without IEEE-mode NaN semantics hipcc drops the canonicalising v_max before each v_min
-# and the min(+inf, x) of the first slot: -5 % instructions in an instruction-fetch-bound loop.  The
-# results for finite inputs are identical (only NaN quieting differs).
-PER_FILE = {"qc.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
+# finite LLRs): with no-NaN semantics hipcc drops the canonicalising v_max before each v_min and the
+# min(+inf, x) of the first slot: -6 % instructions in an instruction-fetch-bound loop.  Results for
+# finite inputs are identical.  (-mno-amdgpu-ieee would also do it, but a kernel whose IEEE-mode
+# attribute differs from the device library's cannot inline any library routine, blockDim included.)
+PER_FILE = {"qc.hip": ["-fno-honor-nans"]}
 
 
-def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), per_file=True) -> str:
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), per_file=True, qc_flags=None) -> str:
     srcs = [os.path.join(HERE, "csrc", s) for s in SRCS]
     deps = srcs + [os.path.join(HERE, "csrc", "common.h"), os.path.join(ROOT, "include", "ldpc_abi.h")]
     deps += [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
     deps.append(os.path.abspath(__file__))
     if not force and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
         return out
+    if qc_flags is not None:
+        PER_FILE["qc.hip"] = qc_flags
     objdir = os.path.join(os.path.dirname(os.path.abspath(out)), "." + os.path.basename(out) + ".objs")
     os.makedirs(objdir, exist_ok=True)
     common = ["hipcc", *[f for f in FLAGS if f != "-shared"], *[f"-D{d}" for d in defines],
@@ -56,5 +59,6 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     out = args[args.index("--out") + 1] if "--out" in args else OUT
     defs = [a[2:] for a in args if a.startswith("-D")]
-    print(build(force="--force" in args or bool(defs) or "--no-per-file" in args, verbose=True, out=out,
-                defines=defs, per_file="--no-per-file" not in args))
+    qcf = next((a.split("=", 1)[1].split() for a in args if a.startswith("--qc-flags=")), None)
+    print(build(force="--force" in args or bool(defs) or "--no-per-file" in args or qcf is not None, verbose=True,
+                out=out, defines=defs, per_file="--no-per-file" not in args, qc_flags=qcf))

@@ -340,11 +340,27 @@ constexpr int edge_off(int r) {
 #define QC_ST_WAVES_PER_SIMD 4  // 128 VGPRs; measured 30.6M cw/s vs 26.2M at 3 waves (648, 50 it)
 #endif
 
-template <class C, bool QUANT, int NORM>
+// Lane-mask rotation for the early-stop syndrome: bit i of the result = bit (i + S) mod Z of x, in each
+// codeword's lane group (CPW == 2: two 27-bit groups at bits 0 and 32).  Wave-uniform: scalar ALU.
+// Bits outside the groups are garbage; the caller masks once per row.
+template <int Z, int CPW, int S>
+__device__ __forceinline__ uint64_t rot_lanes(uint64_t x) {
+    if constexpr (S == 0) {
+        return x;
+    } else if constexpr (CPW == 1) {
+        return (x >> S) ^ (x << (Z - S));
+    } else {
+        const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+        return ((uint64_t)((hi >> S) ^ (hi << (Z - S))) << 32) | (uint32_t)((lo >> S) ^ (lo << (Z - S)));
+    }
+}
+
+template <class C, bool QUANT, bool EARLY, int NORM>
 __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const float* __restrict__ llr, int64_t B, int iters,
                                                                        float clamp, float alpha, float beta, float qmax,
                                                                        float app_max, float qinv, int flags,
-                                                                       uint8_t* __restrict__ bits, float* __restrict__ soft) {
+                                                                       uint8_t* __restrict__ bits, float* __restrict__ soft,
+                                                                       int32_t* __restrict__ iters_used) {
     constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB);
     static_assert(Z <= 64, "register kernel needs Z <= 64");
@@ -382,8 +398,58 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
     float msg[NE];  // c2v of every edge (variable frame); v2c in place during an iteration
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
+    // early stop: lanes of each codeword group, converged groups, their iteration counts
+    constexpr uint64_t ACTIVE = lane_range_mask<Z, CPW>(0, Z);
+    uint64_t done_groups = 0;  // (group lane mask) of converged codewords, CPW == 2
+    int used_lo = iters, used_hi = iters;
 
     for (int it = 0; it < iters; ++it) {
+        if constexpr (EARLY) {
+            if (it > 0) {
+                // syndrome of APP_it: per block column one ballot of the hard decisions (bit = APP <= 2*ZTHR;
+                // quantized: APP < 0, the same for integers), then per check row the XOR of its columns'
+                // masks rotated into the check frame by the edge's lane shift
+                uint64_t par[MB];
+#pragma unroll
+                for (int r = 0; r < MB; ++r) par[r] = 0;
+                const float thr2 = 2.0f * kZthrF32;
+                static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                    constexpr int j = decltype(jj)::value;
+                    const uint64_t b = __ballot(app[j] <= thr2) & ACTIVE;
+                    static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                        constexpr int r = decltype(rr)::value;
+                        constexpr int t = first_slot<C>(r, j);
+                        if constexpr (t >= 0) par[r] ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                    });
+                });
+                uint64_t unsat = 0;
+#pragma unroll
+                for (int r = 0; r < MB; ++r) unsat |= par[r];
+                unsat &= ACTIVE;
+                if constexpr (CPW == 1) {
+                    if (unsat == 0) {  // the wave's codeword satisfies every check: APP_it is the output
+                        used_lo = it;
+                        break;
+                    }
+                } else {
+                    constexpr uint64_t G0 = lane_range_mask<Z, 1>(0, Z), G1 = G0 << 32;
+                    const uint64_t newly = ((unsat & G0) ? 0 : G0) | ((unsat & G1) ? 0 : G1);
+                    const uint64_t fresh = newly & ~done_groups;
+                    if (fresh) {
+                        // park the converged codeword's APP_it in its own L region of LDS (L is no longer
+                        // needed by it); its lanes keep computing for the other codeword, discarded
+                        if (fresh & G0) used_lo = it;
+                        if (fresh & G1) used_hi = it;
+                        if ((fresh >> lane) & 1ull) {
+#pragma unroll
+                            for (int j = 0; j < NB; ++j) Ls[lbase + j * Z] = app[j];
+                        }
+                        done_groups |= fresh;
+                        if (done_groups == (G0 | G1)) break;
+                    }
+                }
+            }
+        }
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
             constexpr int r = decltype(rr)::value;
             static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
@@ -451,16 +517,19 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
     asm volatile("" : "+v"(tid));
     const int zo = (CPW == 2) ? (tid & 31) : (tid & 63);
     const int64_t cwo = (((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0);
+    const bool parked = EARLY && CPW == 2 && ((done_groups >> (tid & 63)) & 1ull);
     if (zo < Z && cwo < B) {
+        const int lbo = ((tid >> 6) * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0)) * N + zo;
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             int t = zo + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const int64_t o = cwo * N + j * Z + t;
-            const float zz = 0.5f * app[j];
+            const float zz = 0.5f * (parked ? Ls[lbo + j * Z] : app[j]);
             if (bits) bits[o] = (uint8_t)(zz <= kZthrF32);
             if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + expf(-zz));
         });
+        if (zo == 0 && iters_used) iters_used[cwo] = (CPW == 2 && ((tid >> 5) & 1)) ? used_hi : used_lo;
     }
 }
 
@@ -627,8 +696,8 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
 #define QL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if (QC_STORED && !E)                                                                                      \
-            k_qc_ms_st<C, true, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf); \
+        if (QC_STORED)                                                                                            \
+            k_qc_ms_st<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
     } while (0)
@@ -639,8 +708,8 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
 #define FL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if (QC_STORED && !E)                                                                                      \
-            k_qc_ms_st<C, false, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf); \
+        if (QC_STORED)                                                                                            \
+            k_qc_ms_st<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
     } while (0)
@@ -654,7 +723,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #undef FL2
 #undef FL
     }
-    if (QC_STORED && !es && used && p.algo != LDPC_ALGO_TANH_SP) fill_i32(used, B, p.iters, st);  // fixed count
+
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
     return LDPC_OK;

@@ -11,6 +11,7 @@ run() {  # name, args...
 }
 rm -f $OUT/bench_configs.jsonl
 run c1_wifi648_minsum50 --steps 22
+run c1_wifi648_tanh50 --steps 11 --algo tanh
 run c1_wifi648_minsum50_generic --steps 11 --force-generic
 run c2_wifi1944_tanh50_16qam --steps 11 --code wifi1944_56 --algo tanh --mod 16qam-ofdm --ebn0 4:0.5:9 --batch 32768
 run c3_wifi1296_q5_20es --steps 11 --code wifi1296_23 --algo qminsum --iters 20 --early-stop --ebn0 0:0.5:5

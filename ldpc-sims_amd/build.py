@@ -37,9 +37,14 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
     common = ["hipcc", *[f for f in FLAGS if f != "-shared"], *[f"-D{d}" for d in defines],
               "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")]
     objs, cmds = [], []
+    hdrs = [d for d in deps if d.endswith(".h")] + [os.path.abspath(__file__)]
     for src in srcs:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
+        # an object is reused when newer than its source, every header and this script (same flags)
+        if (not force and not defines and os.path.exists(out) and os.path.exists(obj)
+                and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in [src, *hdrs])):
+            continue
         cmds.append([*common, *(PER_FILE.get(os.path.basename(src), []) if per_file else []), "-c", "-o", obj, src])
     link = ["hipcc", "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out, *objs]
 
@@ -48,7 +53,7 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
 
-    with ThreadPoolExecutor(max_workers=len(cmds)) as ex:
+    with ThreadPoolExecutor(max_workers=max(1, len(cmds))) as ex:
         list(ex.map(run, cmds))
     run(link)
     return out

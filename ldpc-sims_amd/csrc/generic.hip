@@ -5,9 +5,9 @@
 //     L[n][ldb]      = -llr                         (P0/P1 convention, bp/bp.py:47 negates inside)
 //     v2c[E][ldb]    variable->check message at the reference's CHECK-ORDER edge id (bp/masking.py:84-88)
 //     c2v[E][ldb]    check->variable message (the reference's x tensor, bp/bp.py:46-47)
-// A workgroup owns one check (or one variable) for 256 codewords, so the graph lookups
-// (row_ptr/var_ptr/var_edges at blockIdx.y) are wave-uniform scalar loads and every message access is a
-// fully coalesced 1 KiB row segment.  This is the reference's own two-array flooding dataflow
+// A wave owns one check (or one variable) for 64*V codewords (tile_slot), so the graph lookups
+// (row_ptr/var_ptr/var_edges) are wave-uniform scalar loads and every message access is a fully
+// coalesced row segment of 256 B - 1 KiB.  This is the reference's own two-array flooding dataflow
 // (SURVEY.md §8(d)): per iteration each kernel streams its messages through HBM once, so it is
 // HBM-bound by construction: bytes/cw/iter = 4*E*s + n*s.
 //
@@ -52,6 +52,16 @@ struct VW {
     static constexpr int v16 = 16 / (int)sizeof(T);
     static constexpr int value = (MAXD <= 8) ? v16 : (MAXD <= 16 ? (v16 >= 2 ? v16 / 2 : 1) : 1);
 };
+
+// Tile of a 256-thread workgroup: 2^tpl2 threads (tpl2 in 6..8, whole waves) per node, V codewords per
+// thread, so 256 >> tpl2 nodes per workgroup.  The node index is wave-uniform (readfirstlane), so graph
+// lookups stay scalar loads.  Small cache-resident chunks (generic_decode) use 64 threads x V = 1..4.
+template <int V>
+__device__ __forceinline__ bool tile_slot(int nodes, int tpl2, int64_t B, int& node, int64_t& cw) {
+    node = __builtin_amdgcn_readfirstlane((int)(blockIdx.y << (8 - tpl2)) + (int)(threadIdx.x >> tpl2));
+    cw = (((int64_t)blockIdx.x << tpl2) + (int64_t)(threadIdx.x & ((1u << tpl2) - 1u))) * V;
+    return node < nodes && cw < B;
+}
 
 template <typename T, int V>
 struct Vec {
@@ -159,15 +169,14 @@ __global__ __launch_bounds__(256) void k_used_final(const uint8_t* __restrict__ 
 // duplicate reads): a wave-uniform `if (k < d)` around each load makes hipcc branch around it and
 // drain vmcnt per load (cdna_hip_programming.md §5, load-reduce trap (c)).
 
-template <typename T, int MAXD, bool ES>
+template <typename T, int MAXD, bool ES, int V>
 __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                const T* __restrict__ L, const T* __restrict__ c2v, T* __restrict__ v2c,
                                                int64_t B, int64_t ldb, int first, uint8_t* __restrict__ hb,
-                                               const uint8_t* __restrict__ done) {
-    constexpr int V = VW<T, MAXD>::value;
-    const int v = blockIdx.y;
-    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
-    if (cw >= B) return;
+                                               const uint8_t* __restrict__ done, int nodes, int tpl2) {
+    int v;
+    int64_t cw;
+    if (!tile_slot<V>(nodes, tpl2, B, v, cw)) return;
     if (ES && all_done<V>(done + cw)) return;
     const int a = var_ptr[v];
     const int d = var_ptr[v + 1] - a;
@@ -212,16 +221,15 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
 // Weighted VC + tanh (bp_vc.py:16-27 with input_weight / llr_weight != 1): every target slot sums its own
 // weighted sources, ascending, skipping itself — the masked mm's terms in its k order.  Weights are
 // wave-uniform (scalar loads).  vn_it/lw_it point at this iteration's block (null = ones).
-template <typename T, int MAXD>
+template <typename T, int MAXD, int V>
 __global__ __launch_bounds__(256) void k_vn_spw(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                 const int32_t* __restrict__ wofs, const T* __restrict__ vn_it,
                                                 const T* __restrict__ lw_it, const T* __restrict__ L,
                                                 const T* __restrict__ c2v, T* __restrict__ v2c, int64_t B, int64_t ldb,
-                                                int first) {
-    constexpr int V = VW<T, MAXD>::value;
-    const int v = blockIdx.y;
-    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
-    if (cw >= B) return;
+                                                int first, int nodes, int tpl2) {
+    int v;
+    int64_t cw;
+    if (!tile_slot<V>(nodes, tpl2, B, v, cw)) return;
     const int a = var_ptr[v];
     const int d = var_ptr[v + 1] - a;
     if (d == 0) return;
@@ -256,14 +264,13 @@ __global__ __launch_bounds__(256) void k_vn_spw(const int32_t* __restrict__ var_
         }
 }
 
-template <typename T, int MAXD, bool ES>
+template <typename T, int MAXD, bool ES, int V>
 __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_ptr, const T* __restrict__ v2c,
                                                T* __restrict__ c2v, int64_t B, int64_t ldb, T clamp,
-                                               const uint8_t* __restrict__ done) {
-    constexpr int V = VW<T, MAXD>::value;
-    const int c = blockIdx.y;
-    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
-    if (cw >= B) return;
+                                               const uint8_t* __restrict__ done, int nodes, int tpl2) {
+    int c;
+    int64_t cw;
+    if (!tile_slot<V>(nodes, tpl2, B, c, cw)) return;
     if (ES && all_done<V>(done + cw)) return;
     const int a = row_ptr[c];
     const int d = row_ptr[c + 1] - a;
@@ -296,15 +303,15 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
         }
 }
 
-template <int MAXD, bool ES>
+template <int MAXD, bool ES, int V>
 __global__ __launch_bounds__(256) void k_vn_ms(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                const float* __restrict__ L, const float* __restrict__ c2v,
                                                float* __restrict__ v2c, int64_t B, int64_t ldb, int first,
-                                               uint8_t* __restrict__ hb, const uint8_t* __restrict__ done) {
-    constexpr int V = VW<float, MAXD>::value;
-    const int v = blockIdx.y;
-    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
-    if (cw >= B) return;
+                                               uint8_t* __restrict__ hb, const uint8_t* __restrict__ done, int nodes,
+                                               int tpl2) {
+    int v;
+    int64_t cw;
+    if (!tile_slot<V>(nodes, tpl2, B, v, cw)) return;
     if (ES && all_done<V>(done + cw)) return;
     const int a = var_ptr[v];
     const int d = var_ptr[v + 1] - a;
@@ -342,14 +349,14 @@ __global__ __launch_bounds__(256) void k_vn_ms(const int32_t* __restrict__ var_p
     }
 }
 
-template <int MAXD, bool ES>
+template <int MAXD, bool ES, int V>
 __global__ __launch_bounds__(256) void k_cn_ms(const int32_t* __restrict__ row_ptr, const float* __restrict__ v2c,
                                                float* __restrict__ c2v, int64_t B, int64_t ldb, float clamp,
-                                               float alpha, float beta, const uint8_t* __restrict__ done) {
-    constexpr int V = VW<float, MAXD>::value;
-    const int c = blockIdx.y;
-    const int64_t cw = ((int64_t)blockIdx.x * kTB + threadIdx.x) * V;
-    if (cw >= B) return;
+                                               float alpha, float beta, const uint8_t* __restrict__ done, int nodes,
+                                               int tpl2) {
+    int c;
+    int64_t cw;
+    if (!tile_slot<V>(nodes, tpl2, B, c, cw)) return;
     if (ES && all_done<V>(done + cw)) return;
     const int a = row_ptr[c];
     const int d = row_ptr[c + 1] - a;
@@ -469,9 +476,38 @@ static WsLayout layout(const GenericArgs& g, int64_t B, size_t elem, bool es) {
     return w;
 }
 
+// Cache-resident chunks.  A decode of B codewords may run as consecutive chunks of Bc codewords whose
+// per-iteration working set (L, v2c, c2v: elem * (n + 2E) bytes per codeword) fits the 256 MiB Infinity
+// Cache, so from the second iteration on the message streams are served on-die.  Chunks are independent
+// (codewords never interact), so results do not depend on Bc (tests/test_gpu_parity.py).
+// Measured (profiles/r01/cache_sweep.txt): min-sum (648,1/2) generic 2.45M -> 2.99M cw/s at 192 MB
+// (VN 4.5 -> 6.9 TB/s, CN 5.9 -> 7.3 TB/s effective); no gain where a chunk would need narrow tiles
+// (DVB-S2-size codes: Bc = 64) and a loss for tanh-SP (more launches, no bandwidth to win).  Default:
+// min-sum only, 192 MB, only when chunks keep full wide tiles (Bc >= 1024).  LDPC_CACHE_BUDGET_MB
+// overrides for every algorithm (0 = one pass).
+static int64_t chunk_cw(const GenericArgs& g, int64_t B, const ldpc_params& p) {
+    const size_t elem = (p.flags & LDPC_F_F64) ? 8 : 4;
+    const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
+    const char* env = getenv("LDPC_CACHE_BUDGET_MB");  // read per call: tests and benches vary it
+    int64_t budget, min_bc;
+    if (env) {
+        const long v = atol(env);
+        budget = (int64_t)(v < 0 ? 0 : v) << 20;
+        min_bc = 64;
+    } else {
+        budget = (p.algo == LDPC_ALGO_MIN_SUM) ? (int64_t)192 << 20 : 0;
+        min_bc = 1024;
+    }
+    if (budget == 0) return B;
+    const int64_t per_cw = (int64_t)elem * (g.n + 2 * (int64_t)g.E) + (es ? g.n : 0);
+    const int64_t bc = budget / per_cw / 64 * 64;
+    if (bc < min_bc) return env ? min_bc : B;
+    return bc < B ? bc : B;
+}
+
 size_t generic_workspace(const GenericArgs& g, int64_t B, const ldpc_params& p) {
     const size_t elem = (p.flags & LDPC_F_F64) ? 8 : 4;
-    return layout(g, B, elem, (p.flags & LDPC_F_EARLY_STOP) != 0).total;
+    return layout(g, chunk_cw(g, B, p), elem, (p.flags & LDPC_F_EARLY_STOP) != 0).total;
 }
 
 // One driver for both algorithms: VN and CN kernels per iteration (plus, with early stop, the
@@ -491,7 +527,6 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
     const T clamp = (T)p.clamp;
     const dim3 tb(kTB);
-    auto gxv = [B](int V) { return (unsigned)((B + (int64_t)kTB * V - 1) / ((int64_t)kTB * V)); };
     const unsigned gcw = (unsigned)((B + kTB - 1) / kTB);
     k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb);
     if (ES) {
@@ -502,44 +537,75 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     if (dv < 0 || dc < 0) return set_error(LDPC_EUNSUPPORTED, "node degree > 32 not supported by generic kernels");
     const T* w_vn = wts ? (const T*)wts->vn : nullptr;
     const T* w_lw = wts ? (const T*)wts->lw : nullptr;
+    // tiles: wide (V = VW codewords per thread) when a wave's 64 lanes have >= 64*VW codewords to cover,
+    // else narrow (V = 1); 2^tpl2 threads per node
+    auto tile = [B](int vw, int& V, int& tpl2) {
+        V = (B >= 64 * vw) ? vw : 1;
+        const int64_t lanes = (B + V - 1) / V;
+        tpl2 = lanes > 128 ? 8 : lanes > 64 ? 7 : 6;
+    };
+    auto grid = [B](int V, int tpl2, int nodes) {
+        return dim3((unsigned)((B + ((int64_t)V << tpl2) - 1) / ((int64_t)V << tpl2)),
+                    (unsigned)((nodes + (256 >> tpl2) - 1) / (256 >> tpl2)));
+    };
     for (int it = 0; it < p.iters; ++it) {
         const int first = (it == 0);
         if (!MS && wts) {
             const T* vn_it = w_vn ? w_vn + (int64_t)it * g.W : nullptr;
             const T* lw_it = w_lw ? w_lw + (int64_t)it * g.n : nullptr;
-#define VNW(D)                                                                                                      \
-    k_vn_spw<T, D><<<dim3(gxv(VW<T, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, g.wofs, vn_it, lw_it, L, \
-                                                                 c2v, v2c, B, ldb, first)
+#define VNW1(D, VV) \
+    k_vn_spw<T, D, VV><<<grid(VV, tpl2, g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, g.wofs, vn_it, lw_it, L, c2v, v2c, B, ldb, first, g.n, tpl2)
+#define VNW(D)                                                     \
+    do {                                                           \
+        int V, tpl2;                                               \
+        tile(VW<T, D>::value, V, tpl2);                            \
+        if (V == 1) VNW1(D, 1); else VNW1(D, (VW<T, D>::value));   \
+    } while (0)
             switch (dv) { case 4: VNW(4); break; case 8: VNW(8); break; case 12: VNW(12); break; case 16: VNW(16); break; case 20: VNW(20); break; case 24: VNW(24); break; default: VNW(32); }
 #undef VNW
+#undef VNW1
         } else {
-#define VN(D)                                                                                                      \
+#define VN1(D, VV)                                                                                                  \
     do {                                                                                                           \
         if constexpr (MS)                                                                                          \
-            k_vn_ms<D, ES><<<dim3(gxv(VW<float, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, (const float*)L, \
-                (const float*)c2v, (float*)v2c, B, ldb, first, hb, done);                                         \
+            k_vn_ms<D, ES, VV><<<grid(VV, tpl2, g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, (const float*)L,          \
+                (const float*)c2v, (float*)v2c, B, ldb, first, hb, done, g.n, tpl2);                              \
         else                                                                                                       \
-            k_vn_sp<T, D, ES><<<dim3(gxv(VW<T, D>::value), g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c,   \
-                B, ldb, first, hb, done);                                                                          \
+            k_vn_sp<T, D, ES, VV><<<grid(VV, tpl2, g.n), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, v2c,          \
+                B, ldb, first, hb, done, g.n, tpl2);                                                               \
+    } while (0)
+#define VN(D)                                                      \
+    do {                                                           \
+        int V, tpl2;                                               \
+        tile(VW<T, D>::value, V, tpl2);                            \
+        if (V == 1) VN1(D, 1); else VN1(D, (VW<T, D>::value));     \
     } while (0)
         switch (dv) { case 4: VN(4); break; case 8: VN(8); break; case 12: VN(12); break; case 16: VN(16); break; case 20: VN(20); break; case 24: VN(24); break; default: VN(32); }
 #undef VN
+#undef VN1
         }
         if (ES && it > 0) {  // the oracle tests the syndrome of APP after each iteration >= 1
             k_syndrome<<<dim3((unsigned)((B + 4 * kTB - 1) / (4 * kTB)), g.m), tb, 0, st>>>(g.row_ptr, g.col_idx, hb,
                                                                                           done, unsat, B, ldb);
             k_converge<<<gcw, tb, 0, st>>>(done, unsat, used, B, it);
         }
-#define CN(D)                                                                                                      \
+#define CN1(D, VV)                                                                                                  \
     do {                                                                                                           \
         if constexpr (MS)                                                                                          \
-            k_cn_ms<D, ES><<<dim3(gxv(VW<float, D>::value), g.m), tb, 0, st>>>(g.row_ptr, (const float*)v2c,        \
-                (float*)c2v, B, ldb, p.clamp, p.alpha, p.beta, done);                                              \
+            k_cn_ms<D, ES, VV><<<grid(VV, tpl2, g.m), tb, 0, st>>>(g.row_ptr, (const float*)v2c, (float*)c2v, B, ldb, \
+                p.clamp, p.alpha, p.beta, done, g.m, tpl2);                                                        \
         else                                                                                                       \
-            k_cn_sp<T, D, ES><<<dim3(gxv(VW<T, D>::value), g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp, done); \
+            k_cn_sp<T, D, ES, VV><<<grid(VV, tpl2, g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp, done, g.m, tpl2); \
+    } while (0)
+#define CN(D)                                                      \
+    do {                                                           \
+        int V, tpl2;                                               \
+        tile(VW<T, D>::value, V, tpl2);                            \
+        if (V == 1) CN1(D, 1); else CN1(D, (VW<T, D>::value));     \
     } while (0)
         switch (dc) { case 4: CN(4); break; case 8: CN(8); break; case 12: CN(12); break; case 16: CN(16); break; case 20: CN(20); break; case 24: CN(24); break; default: CN(32); }
 #undef CN
+#undef CN1
     }
     if (p.iters == 0) (void)hipMemsetAsync(c2v, 0, sizeof(T) * (size_t)g.E * ldb, st);
     k_final<T, 32, MS><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, B,
@@ -554,8 +620,26 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     return LDPC_OK;
 }
 
+static int decode_chunk(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,
+                        void* soft, int32_t* iters_used, char* ws, hipStream_t st, const BPWeights* w);
+
 int generic_decode(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,
                    void* soft, int32_t* iters_used, char* ws, hipStream_t st, const BPWeights* w) {
+    const size_t elem = (p.flags & LDPC_F_F64) ? 8 : 4;
+    const int64_t bc = chunk_cw(g, B, p);
+    for (int64_t o = 0; o < B; o += bc) {
+        const int64_t b = (B - o < bc) ? B - o : bc;
+        const int64_t vo = o * g.n;
+        const int rc = decode_chunk(g, (const char*)llr_dev + vo * elem, b, p, bits ? bits + vo : nullptr,
+                                    soft ? (void*)((char*)soft + vo * elem) : nullptr, iters_used ? iters_used + o : nullptr,
+                                    ws, st, w);
+        if (rc != LDPC_OK) return rc;
+    }
+    return LDPC_OK;
+}
+
+static int decode_chunk(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,
+                        void* soft, int32_t* iters_used, char* ws, hipStream_t st, const BPWeights* w) {
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
     if (w && (p.algo != LDPC_ALGO_TANH_SP || es))
         return set_error(LDPC_EUNSUPPORTED, "weighted BP is tanh sum-product without early stop");

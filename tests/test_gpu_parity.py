@@ -282,3 +282,48 @@ def test_qc_sp_equals_generic_sp_bitwise(code, B):
         assert torch.equal(a["soft"].view(torch.int32), b["soft"].view(torch.int32))
     r = dec.decode(x, 30, algo="tanh", clamp=10.0, want_iters=True)
     assert bool((r["iters_used"] == 30).all())
+
+
+@pytest.mark.parametrize("code", ["wifi648_12", "dvbs2s_12"])
+def test_cache_resident_chunks_match_single_pass(code, monkeypatch):
+    """The generic path decodes in Infinity-Cache-sized chunks (LDPC_CACHE_BUDGET_MB).  A tiny budget forces
+    64-codeword chunks (narrow 64-lane tiles) plus a ragged tail; results must equal the single-pass decode
+    bit for bit and the oracle's (min-sum bitwise, early-stop iteration counts included)."""
+    if code == "dvbs2s_12":
+        from ldpc_amd.codes import IRAEncoder, dvbs2_shaped
+        H = dvbs2_shaped()
+        rng = np.random.default_rng(5)
+        cw = IRAEncoder(H).encode(rng.integers(0, 2, size=(133, H.k)))
+        sigma = np.sqrt(1.0 / (2 * 0.5 * 10 ** (1.2 / 10)))
+        llr = (-2.0 * ((1.0 - 2.0 * cw) + sigma * rng.standard_normal(cw.shape)) / sigma**2).astype(np.float32)
+        iters = 6
+    else:
+        H, _ = get_code(code)
+        _, llr = _llr(H, 301, 2.0, seed=41)
+        iters = 20
+    dec = ldpc_amd.get_decoder(H)
+    x = torch.from_numpy(llr).cuda()
+    out = {}
+    for budget in ("0", "1"):
+        monkeypatch.setenv("LDPC_CACHE_BUDGET_MB", budget)
+        out[budget] = [dec.decode(x, iters, algo="minsum", clamp=20.0, early_stop=True, force_generic=True,
+                                  want_iters=True, soft="z"),
+                       dec.decode(x, iters, algo="tanh", clamp=10.0, force_generic=True, soft="p1")]
+    for a, b in zip(out["0"], out["1"]):
+        for k in ("bits", "soft", "iters_used"):
+            if a.get(k) is None:
+                assert b.get(k) is None
+                continue
+            assert torch.equal(a[k].view(torch.int32) if a[k].dtype == torch.float32 else a[k],
+                               b[k].view(torch.int32) if b[k].dtype == torch.float32 else b[k]), k
+    if code == "wifi648_12":
+        ref = oracle.ms_f32(H, llr, iters, 20.0, early_stop=True)
+        r = out["1"][0]
+        assert np.array_equal(r["iters_used"].cpu().numpy(), ref["iters_used"])
+        assert np.array_equal(r["soft"].cpu().numpy().view(np.uint32), ref["z"].view(np.uint32))
+        r64 = dec.decode(llr.astype(np.float64), 5, algo="tanh", clamp=10.0, precision="f64", soft="p1",
+                         force_generic=True)
+        monkeypatch.setenv("LDPC_CACHE_BUDGET_MB", "0")
+        r64b = dec.decode(llr.astype(np.float64), 5, algo="tanh", clamp=10.0, precision="f64", soft="p1",
+                          force_generic=True)
+        assert np.array_equal(r64["soft"], r64b["soft"])

@@ -173,9 +173,10 @@ def test_count_errors_and_awgn():
 
 # ---------------------------------------------------------------- QC register kernel specifics
 QC_CODES = ["wifi648_12", "wifi1296_23"]
+QC_SP_CODES = QC_CODES + ["wifi1944_56"]  # Z = 81: sliced tanh-SP kernel
 
 
-@pytest.mark.parametrize("code", QC_CODES)
+@pytest.mark.parametrize("code", QC_SP_CODES)
 def test_qc_kernel_is_selected(code):
     H, qc = get_code(code)
     assert ldpc_amd.get_decoder(H).qc_z == qc.Z
@@ -262,7 +263,7 @@ def test_generic_early_stop_vs_oracle(code, algo):
     assert (ref["iters_used"] < 20).any()          # the test exercises convergence
 
 
-@pytest.mark.parametrize("code", QC_CODES)
+@pytest.mark.parametrize("code", QC_SP_CODES)
 @pytest.mark.parametrize("B", [1, 1001])
 def test_qc_sp_equals_generic_sp_bitwise(code, B):
     """The on-chip tanh-SP kernel performs the generic kernels' operations in the same order with the

@@ -9,7 +9,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRCS = ["abi.hip", "generic.hip", "qc.hip", "channel.hip"]
+SRCS = ["abi.hip", "generic.hip", "qc.hip", "qc_sl.hip", "channel.hip"]
 OUT = os.path.join(HERE, "ldpc_amd", "libldpc_hip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off",  # min-sum must round exactly like oracle/ldpc_oracle.c (no FMA contraction)
@@ -20,7 +20,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
 # min(+inf, x) of the first slot: -6 % instructions in an instruction-fetch-bound loop.  Results for
 # finite inputs are identical.  (-mno-amdgpu-ieee would also do it, but a kernel whose IEEE-mode
 # attribute differs from the device library's cannot inline any library routine, blockDim included.)
-PER_FILE = {"qc.hip": ["-fno-honor-nans"]}
+PER_FILE = {"qc.hip": ["-fno-honor-nans"], "qc_sl.hip": ["-fno-honor-nans"]}
 
 
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), per_file=True, qc_flags=None) -> str:

@@ -17,10 +17,7 @@
 // normalisation/offset/clamp sequence, same hard-decision rule; so bits and soft outputs are bit-exact.
 // Early stop: the syndrome of APP_it is evaluated for free on the values the next iteration's CN
 // gathers anyway; a codeword whose syndrome is zero is emitted with iters_used = it.
-#include "common.h"
-#include "qc_tables.h"
-
-#include <type_traits>
+#include "qc_common.h"
 
 namespace ldpc {
 
@@ -48,29 +45,6 @@ struct QCSpec {
                      hipStream_t st);
 };
 
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        static_for<B + 1, E>(f);
-    }
-}
-
-// first block row whose checks touch block column j (VN adds start there, so L_j is read there)
-template <class C>
-constexpr int first_row(int j) {
-    for (int r = 0; r < C::MB; ++r)
-        for (int t = 0; t < C::DEG[r]; ++t)
-            if (C::COL[r][t] == j) return r;
-    return -1;
-}
-template <class C>
-constexpr int first_slot(int r, int j) {
-    for (int t = 0; t < C::DEG[r]; ++t)
-        if (C::COL[r][t] == j) return t;
-    return -1;
-}
-
 // lanes whose lifting index z lies in [lo, hi), in each codeword's lane group
 template <int Z, int CPW>
 constexpr uint64_t lane_range_mask(int lo, int hi) {
@@ -89,18 +63,6 @@ __device__ __forceinline__ int sel_lanes(int a, int b) {
     int r;
     asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(MASK));
     return r;
-}
-
-// ms_mag (oracle: min(clamp, max(alpha*m - beta, 0))) specialised on which of alpha != 1 / beta != 0
-// hold: alpha == 1 makes alpha*m exact and beta == 0 makes max(m - 0, 0) == m for m >= 0 (m is a
-// minimum of |v|, never negative), so each form is bit-identical to the general one for its case.
-enum { NORM_PLAIN = 0, NORM_ALPHA = 1, NORM_BETA = 2, NORM_BOTH = 3 };
-template <int NORM>
-__device__ __forceinline__ float mag_of(float m, float alpha, float beta, float clamp) {
-    if constexpr (NORM == NORM_PLAIN) return fminf(m, clamp);
-    else if constexpr (NORM == NORM_ALPHA) return fminf(alpha * m, clamp);
-    else if constexpr (NORM == NORM_BETA) return fminf(fmaxf(m - beta, 0.0f), clamp);
-    else return ms_mag(m, alpha, beta, clamp);
 }
 
 __device__ __forceinline__ float bperm(int addr, float v) {
@@ -329,13 +291,6 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
 // oracle, operation for operation.  The register kernel is instruction-fetch bound (SQC_ICACHE_BUSY ~
 // 100%): this form executes ~12 instead of ~17 instructions (~76 instead of ~124 bytes) per edge, at
 // <= 128 VGPRs (4 waves per SIMD).
-template <class C>
-constexpr int edge_off(int r) {
-    int o = 0;
-    for (int q = 0; q < r; ++q) o += C::DEG[q];
-    return o;
-}
-
 #ifndef QC_ST_WAVES_PER_SIMD
 #define QC_ST_WAVES_PER_SIMD 4  // 128 VGPRs; measured 30.6M cw/s vs 26.2M at 3 waves (648, 50 it)
 #endif
@@ -540,25 +495,6 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
 // continue; per check, p_t = the ascending product skipping t, clamped to +-(1-1e-7), then
 // log((1+p)/(1-p)) clamped to +-clamp; final z = 0.5 * (L + ascending sum).  Same tanhf/logf/expf, so the
 // values equal the generic GPU path's.
-template <class C>
-constexpr int col_deg(int j) {
-    int d = 0;
-    for (int r = 0; r < C::MB; ++r)
-        for (int t = 0; t < C::DEG[r]; ++t) d += (C::COL[r][t] == j);
-    return d;
-}
-template <class C>
-constexpr int col_edge(int j, int k) {  // k-th edge of block column j in ascending row order
-    int c = 0;
-    for (int r = 0; r < C::MB; ++r)
-        for (int t = 0; t < C::DEG[r]; ++t)
-            if (C::COL[r][t] == j) {
-                if (c == k) return edge_off<C>(r) + t;
-                ++c;
-            }
-    return -1;
-}
-
 #ifndef QC_SP_WAVES_PER_SIMD
 #define QC_SP_WAVES_PER_SIMD 4
 #endif
@@ -676,169 +612,9 @@ __global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const fl
     }
 }
 
-// ---- sliced register kernels for Z > 64 (802.11n Z = 81) -----------------------------------------
-// The lifting index is split into S slots of ZL = Z / S <= 32 lanes: a unit of S waves decodes two
-// codewords (lane halves), wave k holding frame positions zc = l + ZL*k of every block column/row.  Each
-// wave keeps its slot's messages in VGPRs; a circulant with rotation rho != 0 moves values between
-// waves, so it is exchanged through LDS: every lane stores its value at positions zc and zc + Z of a
-// per-circulant row [half][2Z] (two copies, so the reader's (zc + rho) mod Z needs no wrap), a barrier,
-// and the reader loads position zc + rho — one base VGPR per lane, every offset an instruction
-// immediate.  Rotation-0 circulants (the lane frames make 30 of 79 so for (1944,5/6)) stay in registers.
-// Per block row: store v2c, barrier, gather, check update, store c2v, barrier, scatter (two buffers).
-template <class C>
-constexpr int nz_count(int r) {  // circulants of row r with a nonzero rotation
-    int c = 0;
-    for (int t = 0; t < C::DEG[r]; ++t) c += (C::SHR[r][t] != 0);
-    return c;
-}
-template <class C>
-constexpr int nz_index(int r, int t) {
-    int c = 0;
-    for (int u = 0; u < t; ++u) c += (C::SHR[r][u] != 0);
-    return c;
-}
-template <class C>
-constexpr int nz_max() {
-    int m = 1;
-    for (int r = 0; r < C::MB; ++r) m = nz_count<C>(r) > m ? nz_count<C>(r) : m;
-    return m;
-}
-
-#ifndef QC_SL_WAVES_PER_SIMD
-#define QC_SL_WAVES_PER_SIMD 3
-#endif
-
-template <class C>
-__global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_SL_WAVES_PER_SIMD)))
-void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
-                uint8_t* __restrict__ bits, float* __restrict__ soft) {
-    constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
-    constexpr int NE = edge_off<C>(MB), NT = nz_max<C>(), ROW = 2 * 2 * Z;  // floats per exchanged circulant
-    static_assert(S > 1 && Z % S == 0 && ZL <= 32, "sliced kernel: Z = S * ZL, ZL <= 32");
-    __shared__ float Xv[NT * ROW], Xc[NT * ROW];
-    const int k = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // slot of this wave
-    const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
-    const int64_t cw = (int64_t)blockIdx.x * 2 + h;
-    const bool live = l < ZL;                // lane carries a frame position
-    const bool valid = live && cw < B;       // ... of a real codeword
-    const int zc = live ? l + ZL * k : 0;    // idle lanes alias position 0 for reads (never store)
-    const int xb = h * 2 * Z + zc;           // this lane's position in an exchange row
-    // L = -llr (bp.py:47) of this lane's variable in every block column, kept in VGPRs
-    float Lr[NB];
-    {
-        const int64_t base = valid ? cw * N : 0;
-        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-            constexpr int j = decltype(jj)::value;
-            int t = zc + C::PHI[j];
-            t -= (t >= Z) ? Z : 0;
-            Lr[j] = valid ? -llr[base + j * Z + t] : 0.0f;
-        });
-    }
-    float msg[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
-    const float pmax = kPmaxF32;
-
-    for (int it = 0; it < iters; ++it) {
-        // VC + tanh in the variable frame (as k_qc_sp_st)
-        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-            constexpr int j = decltype(jj)::value;
-            constexpr int dj = col_deg<C>(j);
-            float P = 0.0f;
-            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
-                constexpr int q = decltype(kk)::value;
-                constexpr int e = col_edge<C>(j, q);
-                float Ssum = P;
-                static_for<q + 1, dj>([&](auto uu) __attribute__((always_inline)) {
-                    Ssum += msg[col_edge<C>(j, decltype(uu)::value)];
-                });
-                const float v = Num<float>::tanh_(0.5f * (Lr[j] + Ssum));
-                P += msg[e];
-                msg[e] = v;
-            });
-        });
-        // CV per block row through the LDS exchange
-        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
-            constexpr int r = decltype(rr)::value;
-            constexpr int d = C::DEG[r];
-            constexpr int e0 = edge_off<C>(r);
-            if (live) {
-                static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                    constexpr int t = decltype(tt)::value;
-                    if constexpr (C::SHR[r][t] != 0) {
-                        constexpr int o = nz_index<C>(r, t) * ROW;
-                        Xv[o + xb] = msg[e0 + t];
-                        Xv[o + xb + Z] = msg[e0 + t];
-                    }
-                });
-            }
-            __syncthreads();
-            float g[d];
-            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                constexpr int t = decltype(tt)::value;
-                constexpr int s = C::SHR[r][t];
-                if constexpr (s == 0) g[t] = msg[e0 + t];
-                else g[t] = Xv[nz_index<C>(r, t) * ROW + xb + s];
-            });
-            float Q = 1.0f;
-            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                constexpr int t = decltype(tt)::value;
-                float p = Q;
-                static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
-                Q *= g[t];
-                if (p > pmax) p = pmax;
-                if (p < -pmax) p = -pmax;
-                float y = Num<float>::log_((1.0f + p) / (1.0f - p));
-                if (y > clamp) y = clamp;
-                if (y < -clamp) y = -clamp;
-                g[t] = y;  // g[t] is not read again (products use u > t)
-            });
-            if (live) {
-                static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                    constexpr int t = decltype(tt)::value;
-                    if constexpr (C::SHR[r][t] != 0) {
-                        constexpr int o = nz_index<C>(r, t) * ROW;
-                        Xc[o + xb] = g[t];
-                        Xc[o + xb + Z] = g[t];
-                    }
-                });
-            }
-            __syncthreads();
-            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                constexpr int t = decltype(tt)::value;
-                constexpr int s = C::SHR[r][t];
-                if constexpr (s == 0) msg[e0 + t] = g[t];
-                else msg[e0 + t] = Xc[nz_index<C>(r, t) * ROW + xb + (Z - s)];
-            });
-        });
-    }
-    if (valid) {
-        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-            constexpr int j = decltype(jj)::value;
-            constexpr int dj = col_deg<C>(j);
-            float Ssum = 0.0f;
-            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) { Ssum += msg[col_edge<C>(j, decltype(kk)::value)]; });
-            const float zz = 0.5f * (Lr[j] + Ssum);
-            int t = zc + C::PHI[j];
-            t -= (t >= Z) ? Z : 0;
-            const int64_t o = cw * N + j * Z + t;
-            if (bits) bits[o] = (uint8_t)Num<float>::bit(zz);
-            if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
-        });
-    }
-}
-
-template <class C>
-static int launch_sl(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
-                     hipStream_t st) {
-    const unsigned blocks = (unsigned)((B + 1) / 2);  // one unit of S waves per codeword pair
-    if (p.algo != LDPC_ALGO_TANH_SP) return set_error(LDPC_EUNSUPPORTED, "sliced QC kernel: tanh-SP only");
-    k_qc_sp_sl<C><<<blocks, C::S * 64, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft);
-    if (used) fill_i32(used, B, p.iters, st);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
-    return LDPC_OK;
-}
+// sliced kernels for Z > 64 (qc_sl.hip)
+int qc_launch_sl_wifi1944_56(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                              int32_t* used, hipStream_t st);
 
 #ifndef QC_STORED
 #define QC_STORED 1  // fixed-iteration launches use k_qc_ms_st
@@ -894,8 +670,8 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 }
 
 #define SPEC(C) {C::MB, C::NB, C::Z, &C::COL[0][0], &C::SH[0][0], &C::DEG[0], C::MAXDC, C::NAME, &launch_ms<C>}
-#define SPEC_SL(C) {C::MB, C::NB, C::Z, &C::COL[0][0], &C::SH[0][0], &C::DEG[0], C::MAXDC, C::NAME, &launch_sl<C>}
-static const QCSpec kSpecs[] = {SPEC(Wifi648_12), SPEC(Wifi1296_23), SPEC_SL(Wifi1944_56)};
+#define SPEC_SL(C, F) {C::MB, C::NB, C::Z, &C::COL[0][0], &C::SH[0][0], &C::DEG[0], C::MAXDC, C::NAME, &F}
+static const QCSpec kSpecs[] = {SPEC(Wifi648_12), SPEC(Wifi1296_23), SPEC_SL(Wifi1944_56, qc_launch_sl_wifi1944_56)};
 #undef SPEC_SL
 #undef SPEC
 
@@ -922,7 +698,6 @@ bool qc_supports(const QCSpec* s, const ldpc_params& p) {
     if (!s) return false;
     if (p.flags & LDPC_F_F64) return false;
     if (p.algo == LDPC_ALGO_TANH_SP) return !(p.flags & LDPC_F_EARLY_STOP);  // on-chip tanh-SP: fixed iterations
-    if (s->z > 64) return false;  // sliced (Z = 81) kernels: tanh-SP only so far
     return p.algo == LDPC_ALGO_MIN_SUM || p.algo == LDPC_ALGO_QMIN_SUM;
 }
 

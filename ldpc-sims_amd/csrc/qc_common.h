@@ -1,0 +1,71 @@
+// qc_common.h — compile-time helpers shared by the quasi-cyclic register kernels (qc.hip, qc_sl.hip).
+#pragma once
+#include "common.h"
+#include "qc_tables.h"
+
+#include <type_traits>
+
+namespace ldpc {
+
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// first block row whose checks touch block column j (VN adds start there, so L_j is read there)
+template <class C>
+constexpr int first_row(int j) {
+    for (int r = 0; r < C::MB; ++r)
+        for (int t = 0; t < C::DEG[r]; ++t)
+            if (C::COL[r][t] == j) return r;
+    return -1;
+}
+template <class C>
+constexpr int first_slot(int r, int j) {
+    for (int t = 0; t < C::DEG[r]; ++t)
+        if (C::COL[r][t] == j) return t;
+    return -1;
+}
+
+// ms_mag (oracle: min(clamp, max(alpha*m - beta, 0))) specialised on which of alpha != 1 / beta != 0
+// hold: alpha == 1 makes alpha*m exact and beta == 0 makes max(m - 0, 0) == m for m >= 0 (m is a
+// minimum of |v|, never negative), so each form is bit-identical to the general one for its case.
+enum { NORM_PLAIN = 0, NORM_ALPHA = 1, NORM_BETA = 2, NORM_BOTH = 3 };
+template <int NORM>
+__device__ __forceinline__ float mag_of(float m, float alpha, float beta, float clamp) {
+    if constexpr (NORM == NORM_PLAIN) return fminf(m, clamp);
+    else if constexpr (NORM == NORM_ALPHA) return fminf(alpha * m, clamp);
+    else if constexpr (NORM == NORM_BETA) return fminf(fmaxf(m - beta, 0.0f), clamp);
+    else return ms_mag(m, alpha, beta, clamp);
+}
+
+template <class C>
+constexpr int edge_off(int r) {
+    int o = 0;
+    for (int q = 0; q < r; ++q) o += C::DEG[q];
+    return o;
+}
+
+template <class C>
+constexpr int col_deg(int j) {
+    int d = 0;
+    for (int r = 0; r < C::MB; ++r)
+        for (int t = 0; t < C::DEG[r]; ++t) d += (C::COL[r][t] == j);
+    return d;
+}
+template <class C>
+constexpr int col_edge(int j, int k) {  // k-th edge of block column j in ascending row order
+    int c = 0;
+    for (int r = 0; r < C::MB; ++r)
+        for (int t = 0; t < C::DEG[r]; ++t)
+            if (C::COL[r][t] == j) {
+                if (c == k) return edge_off<C>(r) + t;
+                ++c;
+            }
+    return -1;
+}
+
+}  // namespace ldpc

@@ -172,8 +172,8 @@ def test_count_errors_and_awgn():
 
 
 # ---------------------------------------------------------------- QC register kernel specifics
-QC_CODES = ["wifi648_12", "wifi1296_23"]
-QC_SP_CODES = QC_CODES + ["wifi1944_56"]  # Z = 81: sliced tanh-SP kernel
+QC_CODES = ["wifi648_12", "wifi1296_23", "wifi1944_56"]  # Z = 81: sliced kernels (qc_sl.hip)
+QC_SP_CODES = QC_CODES
 
 
 @pytest.mark.parametrize("code", QC_SP_CODES)

@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
             constexpr int d = C::DEG[r];
             const uint32_t idx_old = pk[r] >> 27;
             float v[d];
-            float mn1 = __builtin_inff(), mn2 = __builtin_inff();
+            float mn1, mn2;
             uint32_t id = 0, tot = 0;
             uint32_t par = 0;  // bit 31 = parity of the hard decisions of this check's variables
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
@@ -193,11 +193,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
                 float x = a - old;
                 if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
                 v[t] = x;
-                const float m = fabsf(x);
-                mn2 = __builtin_amdgcn_fmed3f(mn1, m, mn2);
-                mn1 = fminf(mn1, m);
                 tot ^= __float_as_uint(x);
             });
+            two_min(v, mn1, mn2);
             if constexpr (early) unsat |= __ballot((int)par < 0);
             between();  // pipelined order: next row's gathers / previous row's adds go here
             tot &= 0x80000000u;
@@ -421,7 +419,7 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
             constexpr int d = C::DEG[r];
             constexpr int e0 = edge_off<C>(r);
             float v[d];
-            float mn1 = __builtin_inff(), mn2 = __builtin_inff();
+            float mn1, mn2;
             uint32_t tot = 0;
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
@@ -434,11 +432,9 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
                     x = bperm(addr, msg[e0 + t]);
                 }
                 v[t] = x;
-                const float m = fabsf(x);
-                mn2 = __builtin_amdgcn_fmed3f(mn1, m, mn2);
-                mn1 = fminf(mn1, m);
                 tot ^= __float_as_uint(x);
             });
+            two_min(v, mn1, mn2);
             tot &= 0x80000000u;
             // sign of the product folded into the two magnitudes once per row
             const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);

@@ -42,6 +42,35 @@ __device__ __forceinline__ float mag_of(float m, float alpha, float beta, float 
     else return ms_mag(m, alpha, beta, clamp);
 }
 
+// The two smallest |v[t]| of a check (multiset order statistics, so any evaluation order gives the same
+// values bit for bit).  Three at a time, then pairs: second(S + {x, y}) = min(mn2, med3(mn1, x, y)), so
+// each pair costs min3 + med3 + min instead of 2 x (med3 + min): fewer code bytes in a loop bound by
+// instruction fetch.  Finite inputs only (no-NaN compile).
+template <int D>
+__device__ __forceinline__ void two_min(const float (&v)[D], float& mn1, float& mn2) {
+    if constexpr (D == 1) {
+        mn1 = fabsf(v[0]);
+        mn2 = __builtin_inff();
+    } else if constexpr (D == 2) {
+        mn1 = fminf(fabsf(v[0]), fabsf(v[1]));
+        mn2 = fmaxf(fabsf(v[0]), fabsf(v[1]));
+    } else {
+        mn1 = fminf(fminf(fabsf(v[0]), fabsf(v[1])), fabsf(v[2]));
+        mn2 = __builtin_amdgcn_fmed3f(fabsf(v[0]), fabsf(v[1]), fabsf(v[2]));
+        static_for<0, (D - 3) / 2>([&](auto pp) __attribute__((always_inline)) {
+            constexpr int t = 3 + 2 * decltype(pp)::value;
+            const float x = fabsf(v[t]), y = fabsf(v[t + 1]);
+            mn2 = fminf(mn2, __builtin_amdgcn_fmed3f(mn1, x, y));
+            mn1 = fminf(fminf(mn1, x), y);
+        });
+        if constexpr ((D - 3) % 2) {
+            const float x = fabsf(v[D - 1]);
+            mn2 = __builtin_amdgcn_fmed3f(mn1, x, mn2);
+            mn1 = fminf(mn1, x);
+        }
+    }
+}
+
 template <class C>
 constexpr int edge_off(int r) {
     int o = 0;

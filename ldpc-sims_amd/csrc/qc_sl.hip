@@ -219,7 +219,7 @@ void k_qc_ms_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
             constexpr int d = C::DEG[r];
             constexpr int e0 = edge_off<C>(r);
             float v[d];
-            float mn1 = __builtin_inff(), mn2 = __builtin_inff();
+            float mn1, mn2;
             uint32_t tot = 0, par = 0;
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
@@ -229,11 +229,9 @@ void k_qc_ms_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 float x = a - msg[e0 + t];
                 if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
                 v[t] = x;
-                const float m = fabsf(x);
-                mn2 = __builtin_amdgcn_fmed3f(mn1, m, mn2);
-                mn1 = fminf(mn1, m);
                 tot ^= __float_as_uint(x);
             });
+            two_min(v, mn1, mn2);
             if constexpr (EARLY) unsat |= __ballot((int)par < 0);
             tot &= 0x80000000u;
             const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);

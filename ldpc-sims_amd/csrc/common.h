@@ -22,16 +22,18 @@ constexpr double kPmaxF64 = 1.0 - 1e-7;
 //   |x| >= 0.625:  1 - 2 / (1 + 2^(2|x| log2 e))  (exp via v_exp_f32 with a split log2e product)
 //   |x| <  0.625:  odd minimax polynomial in x^2
 // sign restored with copysign.  Tests compare it with the generic and the oracle paths.
+// The library's overflow select (2|x| > 88.72: e = inf) is replaced by clamping 2|x| to 100 before the
+// exponential: below 88.72 nothing changes; above it e is >= 2^127 (or inf) either way and the result is
+// 1 - 2 / (1 + e) = 1.0 exactly in both forms, so the output bits are the same for every input.
 __device__ __forceinline__ float tanh_f32(float x) {
     const float ax = fabsf(x);
-    const float t = ax + ax;
+    const float t = fminf(ax + ax, 100.0f);
     const float ph = t * 0x1.715476p+0f;                    // 2|x| * log2(e)
     const float n = __builtin_rintf(ph);
     float lo = __builtin_fmaf(t, 0x1.715476p+0f, -ph);
     lo = __builtin_fmaf(t, 0x1.4ae0bep-26f, lo);
     const float f = (ph - n) + lo;
-    float e = __builtin_ldexpf(__builtin_amdgcn_exp2f(f), (int)n);
-    e = (t > 0x1.62e43p+6f) ? __builtin_inff() : e;         // overflow: 1 - 2/inf = 1
+    const float e = __builtin_ldexpf(__builtin_amdgcn_exp2f(f), (int)n);
     const float big = __builtin_fmaf(__builtin_amdgcn_rcpf(1.0f + e), -2.0f, 1.0f);
     const float x2 = x * x;
     float p = __builtin_fmaf(-0x1.758e7ap-8f, x2, 0x1.521192p-6f);
@@ -40,22 +42,64 @@ __device__ __forceinline__ float tanh_f32(float x) {
     p = __builtin_fmaf(x2, p, -0x1.555532p-2f);
     p = ax * p;
     const float small = __builtin_fmaf(x2, p, ax);
-    return __builtin_copysignf(ax >= 0.625f ? big : small, x);
+    return __builtin_copysignf(t >= 1.25f ? big : small, x);  // t = 2|x| exactly below the clamp
+}
+
+// fp32 division n / d as the device library lowers it (v_div_scale, Newton-Raphson on v_rcp_f32,
+// v_div_fmas, v_div_fixup) with the scaling and fix-up steps dropped.  For normal operands whose
+// exponents differ by far less than 96 — here n, d in [2^-23, 2] — v_div_scale returns its operand,
+// v_div_fmas is a plain fma and v_div_fixup the identity, so the bits are the library's (correctly
+// rounded) quotient; 8 instead of 11 instructions, none of them VCC-writing (no hazard nops).
+__device__ __forceinline__ float div_f32_unscaled(float n, float d) {
+    float r = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    float q = n * r;
+    const float e2 = __builtin_fmaf(-d, q, n);
+    q = __builtin_fmaf(e2, r, q);
+    const float e3 = __builtin_fmaf(-d, q, n);
+    return __builtin_fmaf(e3, r, q);
+}
+
+// logf as the device library computes it (__ocml_log_f32: v_log_f32, then log2 -> ln in extended
+// precision) for NORMAL finite x: the library's denormal prescale and its inf/nan pass-through select
+// never fire there, so this is the same bits in 5 instead of 12 instructions.
+__device__ __forceinline__ float log_f32_normal(float x) {
+    const float r = __builtin_amdgcn_logf(x);
+    const float h = r * 0x1.62e42ep-1f;                 // 0x3f317217
+    float lo = __builtin_fmaf(r, 0x1.62e42ep-1f, -h);
+    lo = __builtin_fmaf(r, 0x1.efa39ep-25f, lo);        // 0x3377d1cf
+    return h + lo;
+}
+
+// Check-node output of the tanh rule for one edge (bp_cv.py:44-50, then the caller's clamp, bp.py:47):
+// p clamped to +-(1-1e-7), y = log((1+p)/(1-p)), clamped to +-clamp.  The clamps are med3 (same values
+// as the two compare-and-set statements for every non-NaN input, -0 included).  fp32: (1+p), (1-p) lie in
+// [2^-23, 2] and their quotient in [2^-24, 2^24], so the restated division and logf above are exact
+// stand-ins for `/` and logf.
+__device__ __forceinline__ float cn_tanh_out(float p, float clamp) {
+    p = __builtin_amdgcn_fmed3f(p, -kPmaxF32, kPmaxF32);
+    const float y = log_f32_normal(div_f32_unscaled(1.0f + p, 1.0f - p));
+    return __builtin_amdgcn_fmed3f(y, -clamp, clamp);
+}
+__device__ __forceinline__ double cn_tanh_out(double p, double clamp) {
+    if (p > kPmaxF64) p = kPmaxF64;
+    if (p < -kPmaxF64) p = -kPmaxF64;
+    double y = log((1.0 + p) / (1.0 - p));
+    if (y > clamp) y = clamp;
+    if (y < -clamp) y = -clamp;
+    return y;
 }
 
 template <typename T> struct Num;
 template <> struct Num<float> {
     __device__ static float tanh_(float x) { return tanh_f32(x); }
-    __device__ static float log_(float x) { return logf(x); }
     __device__ static float exp_(float x) { return expf(x); }
-    static constexpr float pmax = kPmaxF32;
     __device__ static bool bit(float z) { return z <= kZthrF32; }
 };
 template <> struct Num<double> {
     __device__ static double tanh_(double x) { return tanh(x); }
-    __device__ static double log_(double x) { return log(x); }
     __device__ static double exp_(double x) { return exp(x); }
-    static constexpr double pmax = kPmaxF64;
     __device__ static bool bit(double z) { return z < kZthrF64; }
 };
 

@@ -291,12 +291,7 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
 #pragma unroll
                 for (int u = e + 1; u < MAXD; ++u)
                     if (u < d) p *= t[u].x[i];
-                if (p > Num<T>::pmax) p = Num<T>::pmax;
-                if (p < -Num<T>::pmax) p = -Num<T>::pmax;
-                T y = Num<T>::log_((T(1) + p) / (T(1) - p));
-                if (y > clamp) y = clamp;
-                if (y < -clamp) y = -clamp;
-                o.x[i] = y;
+                o.x[i] = cn_tanh_out(p, clamp);  // clamp p, log((1+p)/(1-p)), clamp (common.h)
                 Q.x[i] *= t[e].x[i];
             }
             store_live<T, V, ES>(c2v + (int64_t)(a + e) * ldb + cw, o, done + cw);

@@ -528,7 +528,6 @@ __global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const fl
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
-    const float pmax = kPmaxF32;
 
     for (int it = 0; it < iters; ++it) {
         // VC + tanh in the variable frame: c2v -> v2c in place
@@ -574,11 +573,7 @@ __global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const fl
                 float p = Q;
                 static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
                 Q *= g[t];
-                if (p > pmax) p = pmax;
-                if (p < -pmax) p = -pmax;
-                float y = Num<float>::log_((1.0f + p) / (1.0f - p));
-                if (y > clamp) y = clamp;
-                if (y < -clamp) y = -clamp;
+                const float y = cn_tanh_out(p, clamp);
                 if constexpr (s == 0) {
                     msg[e0 + t] = y;
                 } else {

@@ -64,7 +64,6 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
-    const float pmax = kPmaxF32;
 
     for (int it = 0; it < iters; ++it) {
         // VC + tanh in the variable frame (as k_qc_sp_st)
@@ -113,11 +112,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 float p = Q;
                 static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
                 Q *= g[t];
-                if (p > pmax) p = pmax;
-                if (p < -pmax) p = -pmax;
-                float y = Num<float>::log_((1.0f + p) / (1.0f - p));
-                if (y > clamp) y = clamp;
-                if (y < -clamp) y = -clamp;
+                const float y = cn_tanh_out(p, clamp);
                 g[t] = y;  // g[t] is not read again (products use u > t)
             });
             if (live) {

@@ -174,7 +174,7 @@ def main():
             traffic = None
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # CPU baseline at N=1 only
         cpu = cpu_baseline(H, args, rate)
 
     if rank == 0:

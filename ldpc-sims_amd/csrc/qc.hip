@@ -608,7 +608,7 @@ int qc_launch_sl_wifi1944_56(const void* llr, int64_t B, const ldpc_params& p, u
                               int32_t* used, hipStream_t st);
 
 #ifndef QC_STORED
-#define QC_STORED 1  // fixed-iteration launches use k_qc_ms_st
+#define QC_STORED 1  // min-sum launches use k_qc_ms_st (fixed or early stop); 0: compressed k_qc_ms (A/B builds)
 #endif
 
 template <class C>
@@ -627,7 +627,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
 #define QL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if (QC_STORED)                                                                                            \
+        if constexpr (QC_STORED != 0)                                                                             \
             k_qc_ms_st<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
@@ -639,7 +639,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
 #define FL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if (QC_STORED)                                                                                            \
+        if constexpr (QC_STORED != 0)                                                                             \
             k_qc_ms_st<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \

@@ -63,6 +63,15 @@ __device__ __forceinline__ bool tile_slot(int nodes, int tpl2, int64_t B, int& n
     return node < nodes && cw < B;
 }
 
+// Message streams are read once and written once per iteration: GEN_NT_LOAD / GEN_NT_STORE build
+// variants with non-temporal ("nt") cache policy on them (A/B, scripts/mkvariant.sh).
+#ifndef GEN_NT_LOAD
+#define GEN_NT_LOAD 0
+#endif
+#ifndef GEN_NT_STORE
+#define GEN_NT_STORE 0
+#endif
+
 template <typename T, int V>
 struct Vec {
     T x[V];
@@ -72,11 +81,11 @@ __device__ __forceinline__ Vec<T, V> vload(const T* p) {
     Vec<T, V> r;
     if constexpr (V * sizeof(T) == 16) {
         using U = __attribute__((ext_vector_type(4))) float;
-        const U u = *reinterpret_cast<const U*>(p);
+        const U u = GEN_NT_LOAD ? __builtin_nontemporal_load(reinterpret_cast<const U*>(p)) : *reinterpret_cast<const U*>(p);
         __builtin_memcpy(r.x, &u, 16);
     } else if constexpr (V * sizeof(T) == 8) {
         using U = __attribute__((ext_vector_type(2))) float;
-        const U u = *reinterpret_cast<const U*>(p);
+        const U u = GEN_NT_LOAD ? __builtin_nontemporal_load(reinterpret_cast<const U*>(p)) : *reinterpret_cast<const U*>(p);
         __builtin_memcpy(r.x, &u, 8);
     } else {
 #pragma unroll
@@ -90,12 +99,14 @@ __device__ __forceinline__ void vstore(T* p, const Vec<T, V>& r) {
         using U = __attribute__((ext_vector_type(4))) float;
         U u;
         __builtin_memcpy(&u, r.x, 16);
-        *reinterpret_cast<U*>(p) = u;
+        if constexpr (GEN_NT_STORE) __builtin_nontemporal_store(u, reinterpret_cast<U*>(p));
+        else *reinterpret_cast<U*>(p) = u;
     } else if constexpr (V * sizeof(T) == 8) {
         using U = __attribute__((ext_vector_type(2))) float;
         U u;
         __builtin_memcpy(&u, r.x, 8);
-        *reinterpret_cast<U*>(p) = u;
+        if constexpr (GEN_NT_STORE) __builtin_nontemporal_store(u, reinterpret_cast<U*>(p));
+        else *reinterpret_cast<U*>(p) = u;
     } else {
 #pragma unroll
         for (int i = 0; i < V; ++i) p[i] = r.x[i];

@@ -1,12 +1,18 @@
 #!/bin/bash
-# mkvariant.sh NAME "extra qc.hip flags" : build_variants/NAME.so = the library with qc.hip rebuilt with the flags
+# mkvariant.sh NAME FILE "extra flags" : build_variants/NAME.so = the library with csrc/FILE rebuilt with the
+# extra flags (other objects from the in-tree build; run `python ldpc-sims_amd/build.py` first)
 set -e
 cd "$(dirname "$0")/.."
-name=$1; shift
+name=$1; file=$2; extra=$3
 O=ldpc-sims_amd/ldpc_amd/.libldpc_hip.so.objs
 mkdir -p build_variants/.o_$name
+per=""
+case $file in qc.hip|qc_sl.hip) per="-fno-honor-nans -mllvm --amdgpu-sched-strategy=iterative-ilp";; esac
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function \
-  -fno-honor-nans $1 -I include -I ldpc-sims_amd/csrc -c -o build_variants/.o_$name/qc.hip.o ldpc-sims_amd/csrc/qc.hip
-hipcc --offload-arch=gfx950 -fPIC -shared -o build_variants/$name.so $O/abi.hip.o $O/generic.hip.o $O/qc_sl.hip.o \
-  $O/channel.hip.o build_variants/.o_$name/qc.hip.o
+  $per $extra -I include -I ldpc-sims_amd/csrc -c -o build_variants/.o_$name/$file.o ldpc-sims_amd/csrc/$file
+objs=""
+for f in abi.hip generic.hip qc.hip qc_sl.hip channel.hip; do
+  if [ $f = $file ]; then objs="$objs build_variants/.o_$name/$f.o"; else objs="$objs $O/$f.o"; fi
+done
+hipcc --offload-arch=gfx950 -fPIC -shared -o build_variants/$name.so $objs
 echo build_variants/$name.so

@@ -202,7 +202,11 @@ def main():
             },
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": achieved / peak, "traffic": traffic,
-                         "bytes_per_codeword_model": bpc, "launch_ms": gpu_ms},
+                         "bytes_per_codeword_model": bpc, "launch_ms": gpu_ms,
+                         # measured HBM rate of the launch (PMC traffic / event time): the register/LDS-
+                         # resident QC kernels keep messages on chip, so frac > 1 on the survey's streaming
+                         # model while the bytes actually moved are the llr in / bits out
+                         "traffic_GBps": (traffic / (gpu_ms * 1e-3) / 1e9) if traffic else None},
             "cpu_baseline": cpu,
             "ber": {"ebn0_db": ebn0.tolist(), "coded_ber_info": coded_ber, "coded_bler": coded_bler,
                     "codewords_per_point": int(c[0, 2])},

@@ -495,10 +495,15 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
 #define QC_SP_WAVES_PER_SIMD 4
 #endif
 
-template <class C>
+// Early stop (EARLY): before iteration it >= 1, the hard decisions of z_it = 0.5 * (L + ascending sum of
+// c2v) — the generic VN kernel's hb, same operations — are balloted per block column and rotated into
+// each check's frame on the scalar unit (as k_qc_ms_st); a codeword whose syndrome is zero stops with
+// iters_used = it and its z_it is parked in its own L region of LDS (its lanes keep computing for the
+// wave's other codeword, discarded).  Bitwise equal to the generic path's early stop.
+template <class C, bool EARLY>
 __global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const float* __restrict__ llr, int64_t B, int iters,
                                                                        float clamp, int flags, uint8_t* __restrict__ bits,
-                                                                       float* __restrict__ soft) {
+                                                                       float* __restrict__ soft, int32_t* __restrict__ iters_used) {
     constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB);
     static_assert(Z <= 64, "register kernel needs Z <= 64");
@@ -528,8 +533,65 @@ __global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const fl
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
+    constexpr uint64_t ACTIVE = lane_range_mask<Z, CPW>(0, Z);
+    uint64_t done_groups = 0;  // lane masks of converged codewords (CPW == 2)
+    int used_lo = iters, used_hi = iters;
 
     for (int it = 0; it < iters; ++it) {
+        if constexpr (EARLY) {
+            if (it > 0) {
+                // z of column j from the c2v of the previous iteration (the epilogue's association)
+                auto zcol = [&](auto jj) __attribute__((always_inline)) {
+                    constexpr int j = decltype(jj)::value;
+                    float S = 0.0f;
+                    static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) {
+                        S += msg[col_edge<C>(j, decltype(kk)::value)];
+                    });
+                    int lr = lbase;
+                    asm volatile("" : "+v"(lr));
+                    return 0.5f * (Ls[lr + j * Z] + S);
+                };
+                uint64_t par[MB];
+#pragma unroll
+                for (int r = 0; r < MB; ++r) par[r] = 0;
+                static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                    constexpr int j = decltype(jj)::value;
+                    const uint64_t b = __ballot(Num<float>::bit(zcol(jj))) & ACTIVE;
+                    static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                        constexpr int r = decltype(rr)::value;
+                        constexpr int t = first_slot<C>(r, j);
+                        if constexpr (t >= 0) par[r] ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                    });
+                });
+                uint64_t unsat = 0;
+#pragma unroll
+                for (int r = 0; r < MB; ++r) unsat |= par[r];
+                unsat &= ACTIVE;
+                if constexpr (CPW == 1) {
+                    if (unsat == 0) {  // the wave's codeword converged: its c2v are the output's
+                        used_lo = it;
+                        break;
+                    }
+                } else {
+                    constexpr uint64_t G0 = lane_range_mask<Z, 1>(0, Z), G1 = G0 << 32;
+                    const uint64_t newly = ((unsat & G0) ? 0 : G0) | ((unsat & G1) ? 0 : G1);
+                    const uint64_t fresh = newly & ~done_groups;
+                    if (fresh) {
+                        if (fresh & G0) used_lo = it;
+                        if (fresh & G1) used_hi = it;
+                        if ((fresh >> lane) & 1ull) {
+                            static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                                constexpr int j = decltype(jj)::value;
+                                const float zz = zcol(jj);
+                                Ls[lbase + j * Z] = zz;  // parked z (its L is no longer needed)
+                            });
+                        }
+                        done_groups |= fresh;
+                        if (done_groups == (G0 | G1)) break;
+                    }
+                }
+            }
+        }
         // VC + tanh in the variable frame: c2v -> v2c in place
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
@@ -587,19 +649,21 @@ __global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const fl
     asm volatile("" : "+v"(tid));
     const int zo = (CPW == 2) ? (tid & 31) : (tid & 63);
     const int64_t cwo = (((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0);
+    const bool parked = EARLY && CPW == 2 && ((done_groups >> (tid & 63)) & 1ull);
     if (zo < Z && cwo < B) {
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             constexpr int dj = col_deg<C>(j);
             float S = 0.0f;
             static_for<0, dj>([&](auto kk) __attribute__((always_inline)) { S += msg[col_edge<C>(j, decltype(kk)::value)]; });
-            const float zz = 0.5f * (Ls[lbase + j * Z] + S);
+            const float zz = parked ? Ls[lbase + j * Z] : 0.5f * (Ls[lbase + j * Z] + S);
             int t = zo + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const int64_t o = cwo * N + j * Z + t;
             if (bits) bits[o] = (uint8_t)Num<float>::bit(zz);
             if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
         });
+        if (zo == 0 && iters_used) iters_used[cwo] = (CPW == 2 && ((tid >> 5) & 1)) ? used_hi : used_lo;
     }
 }
 
@@ -620,9 +684,9 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
     const float* x = (const float*)llr;
     float* sf = (float*)soft;
-    if (p.algo == LDPC_ALGO_TANH_SP) {  // qc_supports: fixed iteration count only
-        k_qc_sp_st<C><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf);
-        if (used) fill_i32(used, B, p.iters, st);
+    if (p.algo == LDPC_ALGO_TANH_SP) {
+        if (es) k_qc_sp_st<C, true><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+        else k_qc_sp_st<C, false><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
     } else if (p.algo == LDPC_ALGO_QMIN_SUM) {
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
 #define QL(E, N)                                                                                                  \
@@ -688,7 +752,7 @@ int qc_z(const QCSpec* s) { return s ? s->z : 0; }
 bool qc_supports(const QCSpec* s, const ldpc_params& p) {
     if (!s) return false;
     if (p.flags & LDPC_F_F64) return false;
-    if (p.algo == LDPC_ALGO_TANH_SP) return !(p.flags & LDPC_F_EARLY_STOP);  // on-chip tanh-SP: fixed iterations
+    if (p.algo == LDPC_ALGO_TANH_SP) return s->z <= 64 || !(p.flags & LDPC_F_EARLY_STOP);  // sliced tanh-SP: fixed iterations
     return p.algo == LDPC_ALGO_MIN_SUM || p.algo == LDPC_ALGO_QMIN_SUM;
 }
 

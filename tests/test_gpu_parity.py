@@ -285,6 +285,30 @@ def test_qc_sp_equals_generic_sp_bitwise(code, B):
     assert bool((r["iters_used"] == 30).all())
 
 
+@pytest.mark.parametrize("code", ["wifi648_12", "wifi1296_23"])
+@pytest.mark.parametrize("B", [1, 2, 777])
+def test_qc_sp_early_stop_equals_generic_bitwise(code, B):
+    """tanh-SP with early termination in the register kernel: iteration counts, bits and z equal the
+    generic kernels' (whose counts equal the oracle's, test_generic_early_stop_vs_oracle), including
+    codeword pairs of one wave that stop at different iterations and an odd batch."""
+    H, qc = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, B, 2.0 if rate < 0.6 else 3.5, seed=51 + B, rate=rate)
+    if B > 2:
+        llr[2] = np.float32(-50.0) * (1 - 2 * cw[2])     # converges at the first check
+    dec = ldpc_amd.get_decoder(H)
+    assert dec.qc_z == qc.Z
+    x = torch.from_numpy(llr).cuda()
+    a = dec.decode(x, 20, algo="tanh", clamp=10.0, early_stop=True, want_iters=True, soft="z")
+    b = dec.decode(x, 20, algo="tanh", clamp=10.0, early_stop=True, want_iters=True, soft="z", force_generic=True)
+    assert torch.equal(a["iters_used"], b["iters_used"])
+    assert torch.equal(a["bits"], b["bits"])
+    assert torch.equal(a["soft"].view(torch.int32), b["soft"].view(torch.int32))
+    if B > 2:
+        u = a["iters_used"].cpu().numpy()
+        assert (u < 20).any() and len(np.unique(u)) > 1   # early exits at several iterations
+
+
 @pytest.mark.parametrize("code", ["wifi648_12", "dvbs2s_12"])
 def test_cache_resident_chunks_match_single_pass(code, monkeypatch):
     """The generic path decodes in Infinity-Cache-sized chunks (LDPC_CACHE_BUDGET_MB).  A tiny budget forces

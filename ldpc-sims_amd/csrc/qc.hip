@@ -24,6 +24,12 @@ namespace ldpc {
 #ifndef QC_DIAG_DPP
 #define QC_DIAG_DPP 0
 #endif
+#ifndef QC_DIAG_NO_L
+#define QC_DIAG_NO_L 0
+#endif
+#ifndef QC_L128
+#define QC_L128 1  // lane-major L rows read with ds_read_b128 in the stored min-sum kernel
+#endif
 #ifndef QC_PIPE
 #define QC_PIPE 0  // software-pipelined row order: measured no gain (not latency-bound), kept as an option
 #endif
@@ -334,15 +340,24 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
         t -= (t >= Z) ? Z : 0;
         return cwbase + j * Z + (valid ? t : 0);
     };
+#if QC_L128
+    using f4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int LSTR = lstr<C>(), NG = (NB + 3) / 4;
+    __shared__ __attribute__((aligned(16))) float Ls[256 * LSTR];  // lane-major L rows (qc_common.h lpos)
+    const int lrow = threadIdx.x * LSTR;
+#define LS_AT(row, j) Ls[(row) + lpos<C>(j)]
+#else
     __shared__ float Ls[4 * CPW * N];
-    const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
+    const int lrow = ((threadIdx.x >> 6) * CPW + half) * N + z;
+#define LS_AT(row, j) Ls[(row) + (j) * Z]
+#endif
     float app[NB];
     static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
         constexpr int j = decltype(jj)::value;
         float x = llr[vidx(z, j, C::PHI[j])] * vmask;
         if (QUANT) x = fminf(fmaxf(rintf(x * qinv), -qmax), qmax);
         app[j] = -x;
-        if (z < Z) Ls[lbase + j * Z] = app[j];
+        if (QC_L128 || z < Z) LS_AT(lrow, j) = app[j];
     });
     if (QUANT) {
 #pragma unroll
@@ -394,8 +409,10 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
                         if (fresh & G0) used_lo = it;
                         if (fresh & G1) used_hi = it;
                         if ((fresh >> lane) & 1ull) {
-#pragma unroll
-                            for (int j = 0; j < NB; ++j) Ls[lbase + j * Z] = app[j];
+                            static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                                constexpr int j = decltype(jj)::value;
+                                LS_AT(lrow, j) = app[j];
+                            });
                         }
                         done_groups |= fresh;
                         if (done_groups == (G0 | G1)) break;
@@ -414,10 +431,23 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
             });
         });
         float nap[NB];
+#if QC_L128
+        f4 Lg[NG];
+#endif
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
             constexpr int r = decltype(rr)::value;
             constexpr int d = C::DEG[r];
             constexpr int e0 = edge_off<C>(r);
+#if QC_L128
+            static_for<0, NG>([&](auto gg) __attribute__((always_inline)) {
+                constexpr int g = decltype(gg)::value;
+                if constexpr (lgroup_row<C>(g) == r) {
+                    int lr = lrow;
+                    asm volatile("" : "+v"(lr));  // not hoisted out of the iteration (register budget)
+                    Lg[g] = *static_cast<const f4*>(__builtin_assume_aligned(&Ls[lr + 4 * g], 16));
+                }
+            });
+#endif
             float v[d];
             float mn1, mn2;
             uint32_t tot = 0;
@@ -439,8 +469,10 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
             // sign of the product folded into the two magnitudes once per row
             const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);
             const float M2 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn2, alpha, beta, clamp)) ^ tot);
-            int lr = lbase;
+#if !QC_L128
+            int lr = lrow;
             asm volatile("" : "+v"(lr));
+#endif
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int j = C::COL[r][t], s = C::SHR[r][t];
@@ -455,7 +487,14 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
                     cr = bperm(addr, c);
                 }
                 msg[e0 + t] = cr;
+#if QC_DIAG_NO_L
+                // DIAGNOSTIC BUILD ONLY (wrong results): no per-iteration L reads, to price them
+                if constexpr (first_row<C>(j) == r) nap[j] = 0.0f;
+#elif QC_L128
+                if constexpr (first_row<C>(j) == r) nap[j] = Lg[lpos<C>(j) / 4][lpos<C>(j) % 4];
+#else
                 if constexpr (first_row<C>(j) == r) nap[j] = Ls[lr + j * Z];
+#endif
                 nap[j] = nap[j] + cr;
             });
         });
@@ -470,19 +509,24 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
     const int64_t cwo = (((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0);
     const bool parked = EARLY && CPW == 2 && ((done_groups >> (tid & 63)) & 1ull);
     if (zo < Z && cwo < B) {
+#if QC_L128
+        const int lbo = tid * LSTR;
+#else
         const int lbo = ((tid >> 6) * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0)) * N + zo;
+#endif
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             int t = zo + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const int64_t o = cwo * N + j * Z + t;
-            const float zz = 0.5f * (parked ? Ls[lbo + j * Z] : app[j]);
+            const float zz = 0.5f * (parked ? LS_AT(lbo, j) : app[j]);
             if (bits) bits[o] = (uint8_t)(zz <= kZthrF32);
             if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + expf(-zz));
         });
         if (zo == 0 && iters_used) iters_used[cwo] = (CPW == 2 && ((tid >> 5) & 1)) ? used_hi : used_lo;
     }
 }
+#undef LS_AT
 
 // ---- tanh sum-product, register-resident (the reference's algorithm on-chip) ---------------------
 // Messages in the variable frame, one VGPR per edge (c2v between iterations, v2c inside one).  The

@@ -71,6 +71,36 @@ __device__ __forceinline__ void two_min(const float (&v)[D], float& mn1, float& 
     }
 }
 
+// Lane-major L rows for the register kernels: each lane keeps its NB values of L (or a parked APP) in
+// its own LDS row of lstr() floats, columns ordered by the block row that first needs them
+// (first_row, ties by column), so one ds_read_b128 brings four columns that are consumed together
+// (6 instead of 20-24 LDS reads per iteration at NB = 24).  lstr / 4 is odd: the 16-byte rows of
+// 8 consecutive lanes cover disjoint banks (conflict-free b128 reads).
+template <class C>
+constexpr int lpos(int j) {
+    int p = 0;
+    for (int q = 0; q < C::NB; ++q) {
+        const int fq = first_row<C>(q), fj = first_row<C>(j);
+        p += (fq < fj) || (fq == fj && q < j);
+    }
+    return p;
+}
+template <class C>
+constexpr int lcol(int p) {
+    for (int j = 0; j < C::NB; ++j)
+        if (lpos<C>(j) == p) return j;
+    return -1;
+}
+template <class C>
+constexpr int lstr() {
+    const int s = (C::NB + 3) / 4 * 4;
+    return ((s / 4) % 2) ? s : s + 4;
+}
+template <class C>
+constexpr int lgroup_row(int g) {  // block row at which group g (positions 4g..4g+3) is first needed
+    return first_row<C>(lcol<C>(4 * g));
+}
+
 template <class C>
 constexpr int edge_off(int r) {
     int o = 0;

@@ -27,6 +27,12 @@ namespace ldpc {
 #ifndef QC_DIAG_NO_L
 #define QC_DIAG_NO_L 0
 #endif
+#ifndef QC_DIAG_NOSEL
+#define QC_DIAG_NOSEL 0
+#endif
+#ifndef QC_DIAG_NOCMP
+#define QC_DIAG_NOCMP 0
+#endif
 #ifndef QC_L128
 #define QC_L128 1  // lane-major L rows read with ds_read_b128 in the stored min-sum kernel
 #endif
@@ -66,9 +72,14 @@ constexpr uint64_t lane_range_mask(int lo, int hi) {
 // with no v_cmp (and no VCC hazard).  Volatile: never CSE'd across rows or hoisted out of the loop.
 template <uint64_t MASK>
 __device__ __forceinline__ int sel_lanes(int a, int b) {
+#if QC_DIAG_NOSEL
+    (void)b;  // DIAGNOSTIC BUILD ONLY (wrong results): no wrap select, to price the address selects
+    return a;
+#else
     int r;
     asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(MASK));
     return r;
+#endif
 }
 
 __device__ __forceinline__ float bperm(int addr, float v) {
@@ -450,7 +461,6 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
 #endif
             float v[d];
             float mn1, mn2;
-            uint32_t tot = 0;
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int s = C::SHR[r][t];
@@ -462,10 +472,9 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
                     x = bperm(addr, msg[e0 + t]);
                 }
                 v[t] = x;
-                tot ^= __float_as_uint(x);
             });
             two_min(v, mn1, mn2);
-            tot &= 0x80000000u;
+            const uint32_t tot = xor_all(v) & 0x80000000u;
             // sign of the product folded into the two magnitudes once per row
             const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);
             const float M2 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn2, alpha, beta, clamp)) ^ tot);
@@ -477,7 +486,11 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
                 constexpr int t = decltype(tt)::value;
                 constexpr int j = C::COL[r][t], s = C::SHR[r][t];
                 // |v| == min1 picks the min slot; ties imply min2 == min1 (bit-exact, see k_qc_ms)
+#if QC_DIAG_NOCMP
+                const float mg = M1;  // DIAGNOSTIC BUILD ONLY (wrong results): prices the argmin select
+#else
                 const float mg = (fabsf(v[t]) == mn1) ? M2 : M1;
+#endif
                 const float c = __uint_as_float(__float_as_uint(mg) ^ (__float_as_uint(v[t]) & 0x80000000u));
                 float cr;
                 if constexpr (s == 0) {

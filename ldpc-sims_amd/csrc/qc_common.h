@@ -101,6 +101,19 @@ constexpr int lgroup_row(int g) {  // block row at which group g (positions 4g..
     return first_row<C>(lcol<C>(4 * g));
 }
 
+// XOR of the bit patterns of v[0..D) (the sign of a check's product is its bit 31): three inputs per
+// v_bitop3_b32 (truth table 0x96), half the VALU instructions of a v_xor chain.
+template <int D>
+__device__ __forceinline__ uint32_t xor_all(const float (&v)[D]) {
+    uint32_t t = __float_as_uint(v[0]);
+    static_for<0, (D - 1) / 2>([&](auto pp) __attribute__((always_inline)) {
+        constexpr int k = 1 + 2 * decltype(pp)::value;
+        t = __builtin_amdgcn_bitop3_b32(t, __float_as_uint(v[k]), __float_as_uint(v[k + 1]), 0x96);
+    });
+    if constexpr ((D - 1) % 2) t ^= __float_as_uint(v[D - 1]);
+    return t;
+}
+
 template <class C>
 constexpr int edge_off(int r) {
     int o = 0;

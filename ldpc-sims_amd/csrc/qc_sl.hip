@@ -215,7 +215,7 @@ void k_qc_ms_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
             constexpr int e0 = edge_off<C>(r);
             float v[d];
             float mn1, mn2;
-            uint32_t tot = 0, par = 0;
+            uint32_t par = 0;
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int j = C::COL[r][t], s = C::SHR[r][t];
@@ -224,11 +224,10 @@ void k_qc_ms_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 float x = a - msg[e0 + t];
                 if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
                 v[t] = x;
-                tot ^= __float_as_uint(x);
             });
             two_min(v, mn1, mn2);
             if constexpr (EARLY) unsat |= __ballot((int)par < 0);
-            tot &= 0x80000000u;
+            const uint32_t tot = xor_all(v) & 0x80000000u;
             const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);
             const float M2 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn2, alpha, beta, clamp)) ^ tot);
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {

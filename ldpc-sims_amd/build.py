@@ -9,7 +9,13 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRCS = ["abi.hip", "generic.hip", "qc.hip", "qc_sl.hip", "channel.hip"]
+# (source, object, extra flags): generic_run.hip is compiled once per driver instantiation of the generic
+# decoder (precision x algorithm x early stop) so its kernel templates build in parallel units.
+_RUNS = [("sp32", "float", 0, 0), ("sp32_es", "float", 0, 1), ("sp64", "double", 0, 0), ("sp64_es", "double", 0, 1),
+         ("ms32", "float", 1, 0), ("ms32_es", "float", 1, 1)]
+SRCS = [("abi.hip", "abi.hip.o", []), ("generic.hip", "generic.hip.o", [])] + [
+    ("generic_run.hip", f"generic_run_{n}.o", [f"-DRUN_T={t}", f"-DRUN_MS={ms}", f"-DRUN_ES={es}", f"-DRUN_NAME=generic_run_{n}"])
+    for (n, t, ms, es) in _RUNS] + [("qc.hip", "qc.hip.o", []), ("qc_sl.hip", "qc_sl.hip.o", []), ("channel.hip", "channel.hip.o", [])]
 OUT = os.path.join(HERE, "ldpc_amd", "libldpc_hip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off",  # min-sum must round exactly like oracle/ldpc_oracle.c (no FMA contraction)
@@ -27,7 +33,7 @@ PER_FILE = {"qc.hip": ["-fno-honor-nans", *SCHED], "qc_sl.hip": ["-fno-honor-nan
 
 
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), per_file=True, qc_flags=None) -> str:
-    srcs = [os.path.join(HERE, "csrc", s) for s in SRCS]
+    srcs = [os.path.join(HERE, "csrc", s) for (s, _, _) in SRCS]
     deps = srcs + [os.path.join(HERE, "csrc", "common.h"), os.path.join(ROOT, "include", "ldpc_abi.h")]
     deps += [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
     deps.append(os.path.abspath(__file__))
@@ -41,14 +47,15 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
               "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc")]
     objs, cmds = [], []
     hdrs = [d for d in deps if d.endswith(".h")] + [os.path.abspath(__file__)]
-    for src in srcs:
-        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+    for (name, oname, extra) in SRCS:
+        src = os.path.join(HERE, "csrc", name)
+        obj = os.path.join(objdir, oname)
         objs.append(obj)
         # an object is reused when newer than its source, every header and this script (same flags)
         if (not force and not defines and os.path.exists(out) and os.path.exists(obj)
                 and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in [src, *hdrs])):
             continue
-        cmds.append([*common, *(PER_FILE.get(os.path.basename(src), []) if per_file else []), "-c", "-o", obj, src])
+        cmds.append([*common, *extra, *(PER_FILE.get(name, []) if per_file else []), "-c", "-o", obj, src])
     link = ["hipcc", "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out, *objs]
 
     def run(cmd):

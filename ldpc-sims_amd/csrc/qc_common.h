@@ -76,20 +76,35 @@ __device__ __forceinline__ void two_min(const float (&v)[D], float& mn1, float& 
 // (first_row, ties by column), so one ds_read_b128 brings four columns that are consumed together
 // (6 instead of 20-24 LDS reads per iteration at NB = 24).  lstr / 4 is odd: the 16-byte rows of
 // 8 consecutive lanes cover disjoint banks (conflict-free b128 reads).
+// The orders are tabulated once per code (static constexpr members are evaluated once; the kernels
+// query them thousands of times at compile time).
+template <class C>
+struct LOrder {
+    struct Tab {
+        int pos[64], col[64];
+    };
+    static constexpr Tab make() {
+        Tab t{};
+        int fr[64] = {};
+        for (int j = 0; j < C::NB; ++j) fr[j] = first_row<C>(j);
+        for (int p = 0; p < 64; ++p) t.col[p] = -1;
+        for (int j = 0; j < C::NB; ++j) {
+            int p = 0;
+            for (int q = 0; q < C::NB; ++q) p += (fr[q] < fr[j]) || (fr[q] == fr[j] && q < j);
+            t.pos[j] = p;
+            t.col[p] = j;
+        }
+        return t;
+    }
+    static constexpr Tab T = make();
+};
 template <class C>
 constexpr int lpos(int j) {
-    int p = 0;
-    for (int q = 0; q < C::NB; ++q) {
-        const int fq = first_row<C>(q), fj = first_row<C>(j);
-        p += (fq < fj) || (fq == fj && q < j);
-    }
-    return p;
+    return LOrder<C>::T.pos[j];
 }
 template <class C>
 constexpr int lcol(int p) {
-    for (int j = 0; j < C::NB; ++j)
-        if (lpos<C>(j) == p) return j;
-    return -1;
+    return LOrder<C>::T.col[p];
 }
 template <class C>
 constexpr int lstr() {

@@ -10,9 +10,7 @@ per=""
 case $file in qc.hip|qc_sl.hip) per="-fno-honor-nans -mllvm --amdgpu-sched-strategy=iterative-ilp";; esac
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function \
   $per $extra -I include -I ldpc-sims_amd/csrc -c -o build_variants/.o_$name/$file.o ldpc-sims_amd/csrc/$file
-objs=""
-for f in abi.hip generic.hip qc.hip qc_sl.hip channel.hip; do
-  if [ $f = $file ]; then objs="$objs build_variants/.o_$name/$f.o"; else objs="$objs $O/$f.o"; fi
-done
+objs="build_variants/.o_$name/$file.o"
+for o in $O/*.o; do [ "$(basename $o)" = "$file.o" ] || objs="$objs $o"; done
 hipcc --offload-arch=gfx950 -fPIC -shared -o build_variants/$name.so $objs
 echo build_variants/$name.so

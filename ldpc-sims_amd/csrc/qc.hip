@@ -306,6 +306,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
 // oracle, operation for operation.  The register kernel is instruction-fetch bound (SQC_ICACHE_BUSY ~
 // 100%): this form executes ~12 instead of ~17 instructions (~76 instead of ~124 bytes) per edge, at
 // <= 128 VGPRs (4 waves per SIMD).
+#ifndef QC_ST_TPB
+#define QC_ST_TPB 256  // threads per workgroup of the stored min-sum kernel (whole waves)
+#endif
 #ifndef QC_ST_WAVES_PER_SIMD
 #define QC_ST_WAVES_PER_SIMD 4  // 128 VGPRs; measured 30.6M cw/s vs 26.2M at 3 waves (648, 50 it)
 #endif
@@ -354,11 +357,11 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
 #if QC_L128
     using f4 = __attribute__((ext_vector_type(4))) float;
     constexpr int LSTR = lstr<C>(), NG = (NB + 3) / 4;
-    __shared__ __attribute__((aligned(16))) float Ls[256 * LSTR];  // lane-major L rows (qc_common.h lpos)
+    __shared__ __attribute__((aligned(16))) float Ls[QC_ST_TPB * LSTR];  // lane-major L rows (qc_common.h lpos)
     const int lrow = threadIdx.x * LSTR;
 #define LS_AT(row, j) Ls[(row) + lpos<C>(j)]
 #else
-    __shared__ float Ls[4 * CPW * N];
+    __shared__ float Ls[(QC_ST_TPB / 64) * CPW * N];
     const int lrow = ((threadIdx.x >> 6) * CPW + half) * N + z;
 #define LS_AT(row, j) Ls[(row) + (j) * Z]
 #endif
@@ -738,6 +741,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     constexpr int CPW = (C::Z <= 32) ? 2 : 1;
     const int64_t waves = (B + CPW - 1) / CPW;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
+    const unsigned blocks_st = (unsigned)((waves + QC_ST_TPB / 64 - 1) / (QC_ST_TPB / 64));
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
     const float* x = (const float*)llr;
     float* sf = (float*)soft;
@@ -749,7 +753,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #define QL(E, N)                                                                                                  \
     do {                                                                                                          \
         if constexpr (QC_STORED != 0)                                                                             \
-            k_qc_ms_st<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
+            k_qc_ms_st<C, true, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
     } while (0)
@@ -761,7 +765,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #define FL(E, N)                                                                                                  \
     do {                                                                                                          \
         if constexpr (QC_STORED != 0)                                                                             \
-            k_qc_ms_st<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
+            k_qc_ms_st<C, false, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
     } while (0)

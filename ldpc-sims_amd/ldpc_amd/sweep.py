@@ -125,16 +125,23 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
     return out
 
 
-PKL_KEYS = ("snrdb", "uncoded_ber", "coded_ber", "coded_bler", "uncoded_ber_quantized", "coded_ber_quantized",
-            "coded_bler_quantized", "wmse_quantized")
+# every key evaluate_quantized.py:155-172 writes and plots.py:12-27 reads, in the reference's order
+PKL_KEYS = ("snrdb", "uncoded_ber", "coded_ber", "coded_bler",
+            "uncoded_ber_nn", "coded_ber_nn", "coded_bler_nn",
+            "uncoded_ber_quantized", "coded_ber_quantized", "coded_bler_quantized",
+            "wmse_nn", "wmse_quantized")
 
 
 def save(result: dict, path: str):
-    """``.pkl``: the reference's schema (``evaluate_quantized.py:156-172`` keys snrdb, uncoded_ber,
-    coded_ber, coded_bler and, with the ADC, the ``*_quantized`` / ``wmse_quantized`` keys, as numpy
-    arrays) for plots.py; ``.json``: plain lists."""
+    """``.pkl``: the reference's schema — all 12 keys of ``evaluate_quantized.py:155-172`` as float64
+    numpy arrays of one entry per SNR point, so ``plots.py`` reads the file unchanged.  The ``*_nn`` keys
+    (the NN LLR estimator, out of scope here) and, for a sweep run without ``--adc-bits``, the
+    ``*_quantized`` keys are NaN arrays of the right length (matplotlib skips NaN points).
+    ``.json``: every result field as plain lists."""
     if path.endswith(".pkl"):
-        keep = {kk: np.asarray(result[kk]) for kk in PKL_KEYS if kk in result}
+        npts = len(np.asarray(result["snrdb"]))
+        keep = {kk: (np.asarray(result[kk], dtype=np.float64) if kk in result else np.full(npts, np.nan))
+                for kk in PKL_KEYS}
         with open(path, "wb") as f:
             pickle.dump(keep, f)
     else:

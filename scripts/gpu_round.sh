@@ -6,7 +6,8 @@ OUT=${OUT:-gpurun_out}
 mkdir -p $OUT
 export TMPDIR=/tmp
 STEPS=${STEPS:-22}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+rm -f $OUT/soft_parity.jsonl
+LDPC_PARITY_LOG=$OUT/soft_parity.jsonl timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 echo "pytest rc=$?" >> $OUT/pytest_gpu.log
 tail -3 $OUT/pytest_gpu.log
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; exit 1; }

@@ -206,8 +206,64 @@ def gen_weighted():
     np.savez_compressed(os.path.join(HERE, "bp_weighted_peg64.npz"), H=H, iters=iters, clamp=clamp, **rec)
 
 
+def run_ref_z(H, iters, clamp, llr32, double=False):
+    """The reference forward (bp/bp.py:43-51) with the final VC output z kept: the loop of bp.py:46-47,
+    then z = final_layer[0]([x, -llr]) (bp_vc.py:16-27 with mask_v_final, llr_expander = I) and
+    p1 = -sigmoid(z) + 1 exactly as final_layer + bp.py:51 compute it."""
+    model = BeliefPropagation(H, iters)
+    model.eval()
+    dtype = torch.float64 if double else torch.float32
+    if double:
+        model = model.double()
+    llr = torch.tensor(llr32, dtype=dtype)
+    x = torch.zeros(llr.shape[0], model.layer_size(), dtype=dtype)
+    with torch.no_grad():
+        for layer in model.layers:
+            x = layer([x, -llr]).clamp(-clamp, clamp)
+        z = model.final_layer[0]([x, -llr])
+        p1 = -1 * model.final_layer[1](z) + 1
+    return p1.numpy(), z.numpy()
+
+
+# 802.11n codes through the reference algorithm (the reference accepts any binary H): per code the Eb/N0
+# points and codewords per point.  Memory: the reference's CV forms (B, E, E) temporaries, 16 x 6399^2 x 8 B
+# = 5.2 GB each for (1944,5/6) in fp64.
+WIFI_SP = [("wifi648_12", (1.0, 2.0), 64), ("wifi1296_23", (2.0, 3.0), 16), ("wifi1944_56", (3.0, 4.0), 16)]
+
+
+def gen_wifi_sp():
+    """bp_<code>_sp.npz: reference tanh-SP p1 and z (fp32 module and .double()), 5 iterations, clamp 10."""
+    from ldpc_amd.codes import get_code
+    iters, clamp = 5, 10.0
+    for name, snrs, B in WIFI_SP:
+        H, qc = get_code(name)
+        H = np.asarray(H, dtype=np.int64)
+        enc = Encoder(H)
+        rate = enc.k / H.shape[1]
+        rec = {}
+        for snr in snrs:
+            rng = np.random.default_rng(int(1000 * snr) + H.shape[1])
+            info = rng.integers(0, 2, size=(B, enc.k))
+            cw = enc.encode(info)
+            llr = bpsk_awgn_llr(cw.astype(np.float64), snr, rate, rng)
+            p32, z32 = run_ref_z(H, iters, clamp, llr)
+            p64, z64 = run_ref_z(H, iters, clamp, llr, double=True)
+            tag = f"snr{snr:g}".replace(".", "p")
+            rec[f"llr_{tag}"] = llr
+            rec[f"codeword_{tag}"] = cw.astype(np.uint8)
+            rec[f"p1_f32_{tag}"] = p32.astype(np.float32)
+            rec[f"z_f32_{tag}"] = z32.astype(np.float32)
+            rec[f"p1_f64_{tag}"] = p64
+            rec[f"z_f64_{tag}"] = z64
+            print(name, tag, "bit errors:", int((np.round(p32) != cw).sum()),
+                  "ref f32 vs f64: |dp1| max", float(np.abs(p32 - p64).max()), "|dz| max", float(np.abs(z32 - z64).max()),
+                  flush=True)
+        np.savez_compressed(os.path.join(HERE, f"bp_{name}_sp.npz"), base=qc.base, Z=qc.Z, iters=iters, clamp=clamp,
+                            snrs=np.array(snrs), **rec)
+
+
 if __name__ == "__main__":
-    parts = sys.argv[1:] or ["bp", "adc", "weighted"]
+    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi"]
     for part in parts:
-        {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted}[part]()
+        {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp}[part]()
     print("done")

@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN
+from softparity import _log
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -29,7 +30,10 @@ def test_demod_matches_reference_golden():
     snr = 10 ** (float(d["snr_db"]) / 10)
     llr, sym = ofdm_demod(rx, int(d["ofdm_size"]), 2, snr, want_symbols=True)
     ref = d["llrs"].reshape(-1)
-    assert np.allclose(llr.cpu().numpy(), ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+    got = llr.cpu().numpy().astype(np.float64)
+    rel = float((np.abs(got - ref) / np.maximum(1.0, np.abs(ref))).max())
+    _log({"label": "demod_ofdm qpsk", "kind": "llr_rel_vs_reference", "max": rel})
+    assert rel <= 5e-6   # measured 7.1e-7 (profiles/r02/soft_parity.jsonl): fp32 DFT vs the reference's fp64
     assert np.allclose(sym.cpu().numpy(), d["rx_symbols"].reshape(-1), atol=1e-5)
 
 

@@ -8,6 +8,7 @@ import pytest
 
 import oracle
 from conftest import GOLDEN
+from softparity import _log, check_p1
 
 pytestmark = pytest.mark.gpu
 
@@ -17,10 +18,13 @@ from ldpc_amd import _abi  # noqa: E402
 from ldpc_amd.codes import Encoder, get_code  # noqa: E402
 
 PEG_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_peg64_snr*.npz")))
-# GPU tanhf/logf/expf (ocml) differ from glibc/torch by ulps; near |p| -> 1 the reference's own
-# log((1+p)/(1-p)) amplifies that (its fp32 output is 2.2e-5 from its fp64 output on these files).
-TOL_P1_F32_VS_REF = 2e-5
+# fp32 soft outputs: 1e-5 against the reference's fp64 p1 on its well-conditioned entries
+# (tests/softparity.py); fp64: against the reference's .double() module.
 TOL_P1_F64_VS_REF = 1e-10
+# GPU fp32 z against the C oracle's fp32 z at 8 iterations: the two evaluate the same operations with
+# different tanhf/logf (ocml vs glibc), ulp differences amplified near |p| -> 1 by log((1+p)/(1-p)).
+# Measured maximum 4.4e-5 (wifi1944_56; profiles/r02/soft_parity.jsonl, label "sp_vs_oracle"), DESIGN §4.
+TOL_Z_REL_VS_ORACLE = 1e-4
 
 
 def _llr(H, B, snr_db, seed, rate=0.5):
@@ -43,7 +47,7 @@ def test_sp_f32_matches_reference_golden(path):
     dec = ldpc_amd.get_decoder(d["H"])
     r = dec.decode(torch.from_numpy(d["llr"]).cuda(), int(d["iters"]), algo="tanh", clamp=float(d["clamp"]), soft="p1")
     assert np.array_equal(r["bits"].cpu().numpy(), d["bits_f32"])
-    assert np.abs(r["soft"].cpu().numpy() - d["p1_f32"]).max() <= TOL_P1_F32_VS_REF
+    check_p1("peg64 " + os.path.basename(path)[:-4], r["soft"].cpu().numpy(), d["p1_f32"], d["p1_f64"])
 
 
 @pytest.mark.parametrize("path", PEG_FILES, ids=lambda p: os.path.basename(p))
@@ -73,7 +77,7 @@ def test_belief_propagation_module_matches_reference_golden():
     x = torch.zeros(llr.shape[0], m.layer_size(), device="cuda")
     assert m.layer_size() == 96
     p1 = m(x, llr, 10).cpu().numpy()
-    assert np.abs(p1 - d["p1_f32"]).max() <= TOL_P1_F32_VS_REF
+    check_p1("module peg64_snr2_it10", p1, d["p1_f32"], d["p1_f64"])
     m64 = m.double()
     p64 = m64(x.double(), llr.double(), 10).cpu().numpy()
     assert np.abs(p64 - d["p1_f64"]).max() <= TOL_P1_F64_VS_REF
@@ -87,7 +91,7 @@ def test_wifi648_sp_matches_reference_golden(force_generic):
     for tag in ("snr1", "snr2"):
         r = dec.decode(d[f"llr_{tag}"], 5, algo="tanh", clamp=10.0, soft="p1", force_generic=force_generic)
         assert np.array_equal(r["bits"], np.round(d[f"p1_f32_{tag}"]).astype(np.uint8))
-        assert np.abs(r["soft"] - d[f"p1_f32_{tag}"]).max() <= TOL_P1_F32_VS_REF
+        check_p1(f"wifi648 {tag} generic={force_generic}", r["soft"], d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"])
         r = dec.decode(d[f"llr_{tag}"].astype(np.float64), 5, algo="tanh", clamp=10.0, soft="p1", precision="f64",
                        force_generic=force_generic)
         assert np.abs(r["soft"] - d[f"p1_f64_{tag}"]).max() <= TOL_P1_F64_VS_REF
@@ -125,7 +129,10 @@ def test_sp_hard_bits_vs_oracle(code, force_generic):
     mism = int((r["bits"] != ref["bits"]).sum())
     assert mism == 0, f"{mism} hard-bit mismatches"
     # soft: half-LLR z; ulp-level transcendental differences, amplified near saturation
-    assert np.abs(r["soft"] - ref["z"]).max() <= 2e-3 * max(1.0, np.abs(ref["z"]).max() / 100)
+    rel = float((np.abs(r["soft"].astype(np.float64) - ref["z"]) / np.maximum(1.0, np.abs(ref["z"]))).max())
+    _log({"label": f"sp_vs_oracle {code} generic={force_generic}", "kind": "z_rel_vs_oracle", "max": rel,
+          "tol": TOL_Z_REL_VS_ORACLE})
+    assert rel <= TOL_Z_REL_VS_ORACLE
 
 
 @pytest.mark.parametrize("B", [1, 63, 64, 65, 1000])

@@ -7,6 +7,7 @@ import pytest
 
 import oracle
 from conftest import GOLDEN
+from softparity import _log, check_p1
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -36,7 +37,7 @@ def test_module_weighted_matches_reference(tag):
     x = torch.zeros(llr.shape[0], m.layer_size(), device="cuda")
     p1 = m(x, llr, CLAMP).cpu().numpy()
     ref = D[f"p1_f32_{tag}"]
-    assert np.abs(p1 - ref).max() < 5e-5
+    check_p1(f"weighted peg64 {tag}", p1, ref, D[f"p1_f64_{tag}"])
     assert np.array_equal(np.round(p1), np.round(ref))
     p64 = m.double()(x.double(), llr.double(), CLAMP).cpu().numpy()
     assert np.abs(p64 - D[f"p1_f64_{tag}"]).max() < 1e-10
@@ -60,7 +61,9 @@ def test_weighted_vs_oracle(code):
     r = d.decode(torch.from_numpy(llr).cuda(), iters, algo="tanh", clamp=10.0, soft="z", weights=w)
     o = oracle.sp_f32(g, llr, iters, 10.0, weights={k: v.astype(np.float32) for k, v in w.items()})
     z = r["soft"].cpu().numpy()
-    assert np.abs(z - o["z"]).max() < 2e-3 * max(1.0, np.abs(o["z"]).max())
+    rel = float((np.abs(z.astype(np.float64) - o["z"]) / np.maximum(1.0, np.abs(o["z"]))).max())
+    _log({"label": f"weighted_vs_oracle {code}", "kind": "z_rel_vs_oracle", "max": rel})
+    assert rel < 5e-6   # measured 7.2e-7 (profiles/r02/soft_parity.jsonl)
     close = np.abs(o["z"]) > 1e-3
     assert np.array_equal(r["bits"].cpu().numpy()[close], o["bits"][close])
     r64 = d.decode(llr.astype(np.float64), iters, algo="tanh", clamp=10.0, soft="z", precision="f64", weights=w)

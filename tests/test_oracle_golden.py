@@ -120,3 +120,30 @@ def test_adc_golden_self_consistent():
     rx = d["rx"]
     for i, (b, r) in enumerate(d["agc"]):
         assert np.isclose(d[f"clip_agc{i}"], np.std(rx) * r, rtol=1e-15)
+
+
+WIFI_SP_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_wifi*_sp.npz")))
+
+
+@pytest.mark.parametrize("path", WIFI_SP_FILES, ids=lambda p: os.path.basename(p)[3:-7])
+def test_oracle_wifi_codes_match_reference(path):
+    """(648,1/2), (1296,2/3), (1944,5/6) through the reference module itself (make_golden.py gen_wifi_sp):
+    the oracle's fp64 p1/z follow the reference's .double() to rounding, its fp32 hard bits equal the
+    reference's fp32 hard bits, and its fp32 soft outputs satisfy the soft-parity rule
+    (tests/softparity.py) that the GPU tests apply."""
+    from ldpc_amd.codes import qc_expand
+    from softparity import check_p1, check_z
+    d = np.load(path)
+    H = qc_expand(d["base"], int(d["Z"]))
+    iters, clamp = int(d["iters"]), float(d["clamp"])
+    assert len(WIFI_SP_FILES) == 3
+    for snr in d["snrs"]:
+        tag = f"snr{snr:g}".replace(".", "p")
+        llr = d[f"llr_{tag}"]
+        r64 = oracle.sp_f64(H, llr.astype(np.float64), iters, clamp)
+        assert np.abs(r64["p1"] - d[f"p1_f64_{tag}"]).max() <= TOL_P1_F64
+        assert np.abs(r64["z"] - d[f"z_f64_{tag}"]).max() <= 1e-11
+        r32 = oracle.sp_f32(H, llr, iters, clamp)
+        assert np.array_equal(r32["bits"], np.round(d[f"p1_f32_{tag}"]).astype(np.uint8))
+        check_p1(f"oracle {path}", r32["p1"], d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"])
+        check_z(f"oracle {path}", r32["z"], d[f"z_f32_{tag}"], d[f"z_f64_{tag}"])

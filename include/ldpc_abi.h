@@ -45,11 +45,14 @@ typedef struct {
     int32_t algo;    /* LDPC_ALGO_*                                                          */
     int32_t flags;   /* LDPC_F_*                                                             */
     float clamp;     /* c2v clamp, the reference's clamp_value (bp/bp.py:47)                 */
-    float alpha;     /* min-sum normalisation (1 = plain min-sum)                            */
-    float beta;      /* min-sum offset (float algo) / integer offset (QMIN_SUM)              */
+    float alpha;     /* min-sum normalisation (1 = plain min-sum; QMIN_SUM requires 1)       */
+    float beta;      /* min-sum offset (float algo) / integer offset >= 0 (QMIN_SUM; a
+                        non-integer beta is LDPC_EINVAL there)                               */
     int32_t qmax;    /* QMIN_SUM: message/LLR saturation (15 = 5-bit signed)                 */
     int32_t app_max; /* QMIN_SUM: posterior saturation                                       */
-    float qstep;     /* QMIN_SUM: LLR quantizer step; q = sat(rint(llr / qstep), qmax)       */
+    float qstep;     /* QMIN_SUM: LLR quantizer step; q = sat(rint(llr * (1.0f / qstep)), qmax)
+                        in fp32 (reciprocal multiply, not division: the two can round
+                        differently at .5 boundaries)                                         */
 } ldpc_params;
 
 /* Build a Tanner graph from H in CSR form (rows = checks, ascending columns).  Replaces

@@ -144,6 +144,11 @@ static bool params_valid(const ldpc_params* p) {
     if (p->algo == LDPC_ALGO_QMIN_SUM && (p->qmax < 1 || p->qmax > 127 || p->app_max < p->qmax ||
                                           p->app_max > 32767 || !(p->qstep > 0.0f)))
         return false;
+    // integer offset min-sum: no normalisation, a whole non-negative offset (the kernels and the oracle's
+    // qms work in small integers; a fractional beta would silently truncate)
+    if (p->algo == LDPC_ALGO_QMIN_SUM && (p->alpha != 1.0f || !(p->beta >= 0.0f) || p->beta != floorf(p->beta) ||
+                                          p->beta > (float)p->qmax))
+        return false;
     return true;
 }
 

@@ -544,6 +544,245 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
 }
 #undef LS_AT
 
+// ---- Phased stored-message min-sum (k_qc_ms_ph) ---------------------------------------------------
+// The same flooding arithmetic as k_qc_ms_st (and the oracle), operation for operation, regrouped into
+// two phases per iteration so that no lane rotation sits on a dependency chain:
+//   CN phase, row by row:   msg[e] (v2c, variable frame) -> gathered into the check frame IN PLACE,
+//                           two-minimum / sign product, msg[e] = new c2v in the CHECK frame.
+//                           Rows are independent: row r+1's gathers overlap row r's arithmetic.
+//   VN phase, column by column: msg[e] -> rotated back to the variable frame in place,
+//                           APP_j = L_j + sum of c2v in ascending row order (the oracle's order),
+//                           msg[e] = APP_j - c2v (v2c of the next iteration).  Columns are independent.
+// Nothing but msg[] is live across a phase (APP is per column and transient), so the rotation
+// addresses — one per distinct lane shift rho, "read lane (z + rho) mod Z of my group" — are computed
+// once before the loop and held in registers (QC_PH_ADDR_MIN_USES) instead of one v_cndmask per ds_bpermute.
+// Iteration 0's v2c is L itself (c2v = +0: L - 0 == L bitwise, also for L = -0), so the loop starts at
+// the CN phase; the last iteration's VN phase writes the outputs directly instead of forming v2c.
+#ifndef QC_PH_ADDR_MIN_USES
+#define QC_PH_ADDR_MIN_USES 3  // rotations used >= 3 times per iteration get an address register (A/B: 1 -> spills, 38.5 vs 37.9 M cw/s at 1; 4: 38.3; 6: 37.7; none: 37.0)
+#endif
+#ifndef QC_PH_WAVES_PER_SIMD
+#define QC_PH_WAVES_PER_SIMD 4
+#endif
+
+template <class C>
+constexpr int rot_uses(int rho) {  // ds_bpermutes per iteration that read lane (z + rho) mod Z
+    int n = 0;
+    for (int r = 0; r < C::MB; ++r)
+        for (int t = 0; t < C::DEG[r]; ++t) {
+            const int s = C::SHR[r][t];
+            n += (s != 0 && (s == rho || C::Z - s == rho));
+        }
+    return n;
+}
+
+template <class C, bool QUANT, bool EARLY, int NORM>
+__global__ __launch_bounds__(256, QC_PH_WAVES_PER_SIMD) void k_qc_ms_ph(const float* __restrict__ llr, int64_t B, int iters,
+                                                                       float clamp, float alpha, float beta, float qmax,
+                                                                       float app_max, float qinv, int flags,
+                                                                       uint8_t* __restrict__ bits, float* __restrict__ soft,
+                                                                       int32_t* __restrict__ iters_used) {
+    constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
+    constexpr int NE = edge_off<C>(MB);
+    static_assert(Z <= 32, "phased kernel: two codewords per wave (Z <= 32)");
+    constexpr int CPW = 2;
+    const int lane = threadIdx.x & 63;
+    const int half = lane >> 5;
+    const int z = lane & 31;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t cw = wave * CPW + half;
+    const bool valid = (z < Z) && (cw < B);
+    const int zb = (z < Z) ? z : z - Z;
+    const int base4 = (half * 32 + zb) * 4;
+    const int base4m = base4 - 4 * Z;
+    using f4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int LSTR = lstr<C>();
+    __shared__ __attribute__((aligned(16))) float Ls[QC_ST_TPB * LSTR];  // lane-major L rows (qc_common.h lpos)
+    const int lrow = threadIdx.x * LSTR;
+
+    // rotation addresses, one register per distinct shift used often enough (the others: one v_cndmask
+    // per use, as k_qc_ms_st)
+    int ra[Z];
+    static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
+        constexpr int rho = decltype(rr)::value;
+        if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES)
+            ra[rho] = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(base4, base4m) + 4 * rho;
+    });
+    auto rot = [&](auto rr, float x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
+        constexpr int rho = decltype(rr)::value;
+        if constexpr (rho == 0) {
+            return x;
+        } else if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES) {
+            return bperm(ra[rho], x);
+        } else {
+            return bperm(sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(base4, base4m) + 4 * rho, x);
+        }
+    };
+    (void)ra;
+
+    // L = -llr (quantized in QUANT mode) into this lane's LDS row; msg = v2c of iteration 0 = APP_0 = L
+    float msg[NE];
+    {
+        const int64_t cwbase = valid ? cw * N : 0;
+        const float vmask = valid ? 1.0f : 0.0f;
+        float L[NB];
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            int t = z + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            float x = llr[cwbase + j * Z + (valid ? t : 0)] * vmask;
+            if (QUANT) x = fminf(fmaxf(rintf(x * qinv), -qmax), qmax);
+            L[j] = -x;
+            Ls[lrow + lpos<C>(j)] = L[j];
+            if (QUANT) L[j] = fminf(fmaxf(L[j], -app_max), app_max);  // APP_0 (k_qc_ms_st: app clamp)
+        });
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                float x = L[C::COL[r][t]] - 0.0f;  // v2c = APP_0 - c2v(= +0), as k_qc_ms_st
+                if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
+                msg[edge_off<C>(r) + t] = x;
+            });
+        });
+    }
+    constexpr uint64_t ACTIVE = lane_range_mask<Z, CPW>(0, Z);
+    constexpr uint64_t G0 = lane_range_mask<Z, 1>(0, Z), G1 = G0 << 32;
+    uint64_t done_groups = 0;
+    int used_lo = iters, used_hi = iters;
+    const float thr2 = 2.0f * kZthrF32;
+
+    // CN phase: v2c (variable frame) -> c2v (check frame), in place
+    auto cn_phase = [&]() __attribute__((always_inline)) {
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            constexpr int d = C::DEG[r];
+            constexpr int e0 = edge_off<C>(r);
+            float v[d];
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                v[t] = rot(std::integral_constant<int, C::SHR[r][t]>{}, msg[e0 + t]);
+            });
+            float mn1, mn2;
+            two_min(v, mn1, mn2);
+            const uint32_t tot = xor_all(v) & 0x80000000u;
+            const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);
+            const float M2 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn2, alpha, beta, clamp)) ^ tot);
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                const float mg = (fabsf(v[t]) == mn1) ? M2 : M1;
+                msg[e0 + t] = __uint_as_float(__float_as_uint(mg) ^ (__float_as_uint(v[t]) & 0x80000000u));
+            });
+        });
+    };
+    // VN phase, column j: c2v back to the variable frame, APP_j = L_j + ascending sum; returns APP_j
+    f4 Lg;
+    auto vn_col = [&](auto pp) __attribute__((always_inline)) {
+        constexpr int p = decltype(pp)::value;  // LDS position (columns in first-use order)
+        constexpr int j = lcol<C>(p);
+        constexpr int dj = col_deg<C>(j);
+        if constexpr (p % 4 == 0) {
+            int lr = lrow;
+            asm volatile("" : "+v"(lr));  // not hoisted out of the loop (register budget)
+            Lg = *static_cast<const f4*>(__builtin_assume_aligned(&Ls[lr + p], 16));
+        }
+        float a = Lg[p % 4];
+        static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int e = col_edge<C>(j, decltype(kk)::value);
+            constexpr int r = edge_row<C>(e), t = e - edge_off<C>(r);
+            constexpr int s = C::SHR[r][t];
+            msg[e] = rot(std::integral_constant<int, (s == 0) ? 0 : Z - s>{}, msg[e]);
+            a = a + msg[e];
+        });
+        if (QUANT) a = fminf(fmaxf(a, -app_max), app_max);
+        return a;
+    };
+    auto v2c_col = [&](auto jj, float a) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int e = col_edge<C>(j, decltype(kk)::value);
+            float x = a - msg[e];
+            if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
+            msg[e] = x;
+        });
+    };
+
+    int it = 0;
+    for (; it + 1 < iters; ++it) {
+        cn_phase();
+        if constexpr (EARLY) {
+            // APP_{it+1} of every column (kept until the syndrome verdict), hard-decision ballots
+            float app[NB];
+            uint64_t par[MB];
+#pragma unroll
+            for (int r = 0; r < MB; ++r) par[r] = 0;
+            static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
+                constexpr int p = decltype(pp)::value;
+                constexpr int j = lcol<C>(p);
+                app[j] = vn_col(pp);
+                const uint64_t b = __ballot(app[j] <= thr2) & ACTIVE;
+                static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                    constexpr int r = decltype(rr)::value;
+                    constexpr int t = first_slot<C>(r, j);
+                    if constexpr (t >= 0) par[r] ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                });
+            });
+            uint64_t unsat = 0;
+#pragma unroll
+            for (int r = 0; r < MB; ++r) unsat |= par[r];
+            unsat &= ACTIVE;
+            const uint64_t newly = ((unsat & G0) ? 0 : G0) | ((unsat & G1) ? 0 : G1);
+            const uint64_t fresh = newly & ~done_groups;
+            if (fresh) {
+                // park the converged codeword's APP in its L row (L is no longer needed by it)
+                if (fresh & G0) used_lo = it + 1;
+                if (fresh & G1) used_hi = it + 1;
+                if ((fresh >> lane) & 1ull) {
+                    static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                        constexpr int j = decltype(jj)::value;
+                        Ls[lrow + lpos<C>(j)] = app[j];
+                    });
+                }
+                done_groups |= fresh;
+                if (done_groups == (G0 | G1)) break;
+            }
+            static_for<0, NB>([&](auto jj) __attribute__((always_inline)) { v2c_col(jj, app[decltype(jj)::value]); });
+        } else {
+            static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
+                constexpr int p = decltype(pp)::value;
+                v2c_col(std::integral_constant<int, lcol<C>(p)>{}, vn_col(pp));
+            });
+        }
+    }
+    // last iteration (or early exit): outputs straight from the VN phase, column by column
+    const bool early_exit = EARLY && done_groups == (G0 | G1);
+    if (!early_exit && iters > 0) cn_phase();
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int zo = tid & 31;
+    const int64_t cwo = (((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + ((tid >> 5) & 1);
+    const bool parked = EARLY && ((done_groups >> (tid & 63)) & 1ull);
+    const bool ok = zo < Z && cwo < B;
+    static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
+        constexpr int p = decltype(pp)::value;
+        constexpr int j = lcol<C>(p);
+        float a;
+        if (iters > 0 && !early_exit) a = vn_col(pp);
+        else a = Ls[lrow + p];  // iters == 0: APP_0 = L (QUANT: clamped below); early exit: parked APP
+        if (QUANT && iters == 0) a = fminf(fmaxf(a, -app_max), app_max);
+        if (parked) a = Ls[lrow + p];
+        if (ok) {
+            int t = zo + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            const int64_t o = cwo * N + j * Z + t;
+            const float zz = 0.5f * a;
+            if (bits) bits[o] = (uint8_t)(zz <= kZthrF32);
+            if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + expf(-zz));
+        }
+    });
+    if (ok && zo == 0 && iters_used) iters_used[cwo] = ((tid >> 5) & 1) ? used_hi : used_lo;
+}
+
 // ---- tanh sum-product, register-resident (the reference's algorithm on-chip) ---------------------
 // Messages in the variable frame, one VGPR per edge (c2v between iterations, v2c inside one).  The
 // operation order is the oracle's and the generic kernels' (bp_vc.py:16-27, bp_cv.py:22-50): per
@@ -734,6 +973,9 @@ int qc_launch_sl_wifi1944_56(const void* llr, int64_t B, const ldpc_params& p, u
 #ifndef QC_STORED
 #define QC_STORED 1  // min-sum launches use k_qc_ms_st (fixed or early stop); 0: compressed k_qc_ms (A/B builds)
 #endif
+#ifndef QC_PHASED
+#define QC_PHASED 1  // Z <= 32 min-sum: the phased kernel k_qc_ms_ph (0: k_qc_ms_st, A/B builds)
+#endif
 
 template <class C>
 static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
@@ -752,7 +994,9 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
 #define QL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if constexpr (QC_STORED != 0)                                                                             \
+        if constexpr (QC_PHASED != 0 && C::Z <= 32)                                                             \
+            k_qc_ms_ph<C, true, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
+        else if constexpr (QC_STORED != 0)                                                                        \
             k_qc_ms_st<C, true, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
@@ -764,7 +1008,9 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
 #define FL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if constexpr (QC_STORED != 0)                                                                             \
+        if constexpr (QC_PHASED != 0 && C::Z <= 32)                                                             \
+            k_qc_ms_ph<C, false, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
+        else if constexpr (QC_STORED != 0)                                                                        \
             k_qc_ms_st<C, false, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \

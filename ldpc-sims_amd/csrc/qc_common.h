@@ -137,6 +137,13 @@ constexpr int edge_off(int r) {
 }
 
 template <class C>
+constexpr int edge_row(int e) {  // block row of (check-order) edge e
+    int r = 0;
+    while (r + 1 < C::MB && edge_off<C>(r + 1) <= e) ++r;
+    return r;
+}
+
+template <class C>
 constexpr int col_deg(int j) {
     int d = 0;
     for (int r = 0; r < C::MB; ++r)

@@ -109,8 +109,10 @@ class Decoder:
                precision="f32", soft=None, qmax=15, app_max=127, qstep=1.0, force_generic=False, stream=None,
                want_bits=True, want_iters=False, weights=None):
         """Decode a (B, n) batch of LLRs (log P1/P0).  numpy in -> numpy out (host staging inside the
-        library); torch GPU tensor in -> torch GPU tensors out, asynchronous on ``stream`` (default: the
-        current torch stream) with a torch-allocated workspace.  Returns dict(bits, soft, iters_used).
+        library); torch GPU tensor in (on this decoder's device) -> torch GPU tensors out, asynchronous on
+        ``stream`` (a ``torch.cuda.Stream``; default: the current stream; a side stream first waits for the
+        current one, and the outputs are allocated on and ordered by the side stream) with a
+        torch-allocated workspace.  Returns dict(bits, soft, iters_used).
         ``weights``: weighted BP (tanh-SP only), compact layout of ``Graph.compact_weights``."""
         is_torch = type(llr).__module__.startswith("torch")
         on_gpu = is_torch and llr.is_cuda
@@ -128,23 +130,34 @@ class Decoder:
                                                  *args[2:])
         if on_gpu:
             torch = _torch()
+            if llr.device.index != self.device:
+                raise ValueError(f"llr is on {llr.device}, this decoder's graph is on cuda:{self.device}")
+            cur = torch.cuda.current_stream(llr.device)
+            ext = cur if stream is None else stream
+            if not isinstance(ext, torch.cuda.Stream):
+                raise TypeError("stream must be a torch.cuda.Stream (or None: the current stream)")
+            if ext != cur:
+                ext.wait_stream(cur)        # llr (and the caller's prior work) is ordered before the decode
+                llr.record_stream(ext)      # the caller's llr stays allocated until the decode has read it
             tdt = torch.float64 if precision == "f64" else torch.float32
-            x = llr.detach().to(tdt).contiguous()
-            if x.dim() != 2 or x.shape[1] != self.n:
-                raise RuntimeError(f"llr must be (B, {self.n}), got {tuple(x.shape)}")
-            B = x.shape[0]
-            dev = x.device
-            bits = torch.empty((B, self.n), dtype=torch.uint8, device=dev) if want_bits else None
-            sft = torch.empty((B, self.n), dtype=tdt, device=dev) if soft else None
-            used = torch.empty((B,), dtype=torch.int32, device=dev) if want_iters else None
-            wsb = self.workspace_bytes(B, p)
-            ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dev)
-            st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-            check(call(x.data_ptr(), B, bits.data_ptr() if bits is not None else None,
-                       sft.data_ptr() if sft is not None else None,
-                       used.data_ptr() if used is not None else None, ws.data_ptr(), wsb, ctypes.c_void_p(st)))
-            # ws was allocated on the current stream; returning it keeps it alive until the caller drops the
-            # result (torch's allocator then recycles it in stream order).
+            # conversion, outputs and workspace all live on the decode stream: the allocator recycles them in
+            # that stream's order, and results are ready once `ext` reaches this point
+            with torch.cuda.stream(ext):
+                x = llr.detach().to(tdt).contiguous()
+                if x.dim() != 2 or x.shape[1] != self.n:
+                    raise RuntimeError(f"llr must be (B, {self.n}), got {tuple(x.shape)}")
+                B = x.shape[0]
+                dev = x.device
+                bits = torch.empty((B, self.n), dtype=torch.uint8, device=dev) if want_bits else None
+                sft = torch.empty((B, self.n), dtype=tdt, device=dev) if soft else None
+                used = torch.empty((B,), dtype=torch.int32, device=dev) if want_iters else None
+                wsb = self.workspace_bytes(B, p)
+                ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dev)
+                check(call(x.data_ptr(), B, bits.data_ptr() if bits is not None else None,
+                           sft.data_ptr() if sft is not None else None,
+                           used.data_ptr() if used is not None else None, ws.data_ptr(), wsb,
+                           ctypes.c_void_p(ext.cuda_stream)))
+            # ws is returned with the outputs so it stays alive until the caller drops the result
             return dict(bits=bits, soft=sft, iters_used=used, workspace=ws)
         if is_torch:
             llr = llr.detach().cpu().numpy()
@@ -186,8 +199,11 @@ def get_decoder(H, device: int = 0) -> Decoder:
 def decode(H, llr, max_iters: int, *, algo="tanh", clamp=10.0, alpha=1.0, beta=0.0, early_stop=False,
            precision="f32", out="bits", device=None, **kw):
     """``decode(H, llr, max_iters)`` -> hard bits (uint8, (B, n)); ``out="bits+soft"`` -> (bits, p1)."""
+    on_gpu = type(llr).__module__.startswith("torch") and llr.is_cuda
     if device is None:
-        device = llr.device.index if (type(llr).__module__.startswith("torch") and llr.is_cuda) else 0
+        device = llr.device.index if on_gpu else 0
+    elif on_gpu and int(device) != llr.device.index:
+        raise ValueError(f"device={device} but llr is on {llr.device}")
     dec = get_decoder(H, device or 0)
     soft = "p1" if out == "bits+soft" else kw.pop("soft", None)
     r = dec.decode(llr, max_iters, algo=algo, clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop,

@@ -359,3 +359,35 @@ def test_cache_resident_chunks_match_single_pass(code, monkeypatch):
         r64b = dec.decode(llr.astype(np.float64), 5, algo="tanh", clamp=10.0, precision="f64", soft="p1",
                           force_generic=True)
         assert np.array_equal(r64["soft"], r64b["soft"])
+
+
+def test_side_stream_and_device_checks():
+    """decode(stream=side) is ordered after the producer on the current stream and equals the default-stream
+    decode; a device mismatch raises instead of launching on foreign pointers."""
+    H, _ = get_code("wifi648_12")
+    cw, llr = _llr(H, 300, 2.0, seed=8)
+    dec = ldpc_amd.get_decoder(H)
+    src = torch.from_numpy(llr).cuda()
+    want = dec.decode(src, 10, algo="minsum", clamp=20.0, soft="z")
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        x = src * 1.0                      # produced on the current stream just before the decode
+        r = dec.decode(x, 10, algo="minsum", clamp=20.0, soft="z", stream=side)
+        del x                              # recycled only after the side stream has read it
+        side.synchronize()
+        assert torch.equal(r["bits"], want["bits"]) and torch.equal(r["soft"], want["soft"])
+    with pytest.raises(TypeError):
+        dec.decode(src, 10, stream=side.cuda_stream)
+    with pytest.raises(ValueError):
+        ldpc_amd.decode(H, src, 5, device=src.device.index + 1)
+
+
+def test_quantized_minsum_rejects_fractional_offset_and_alpha():
+    """QMIN_SUM is integer offset min-sum: beta must be a whole number and alpha 1 (ldpc_abi.h)."""
+    H, _ = get_code("wifi648_12")
+    dec = ldpc_amd.get_decoder(H)
+    x = torch.zeros((4, 648), device="cuda")
+    for kw in (dict(beta=0.5), dict(alpha=0.75), dict(beta=-1.0)):
+        with pytest.raises(_abi.LdpcError):
+            dec.decode(x, 3, algo="qminsum", **kw)
+    dec.decode(x, 3, algo="qminsum", beta=1.0)

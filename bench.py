@@ -56,7 +56,8 @@ def main():
                     help="LLR generator (outside the timed region): BPSK/AWGN or the OFDM front end")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--counters-json", default=os.path.join(ROOT, "profiles", "counters.json"),
+                    help="per-launch PMC counts per configuration (scripts/gpu_profile.sh + counters_summary.py)")
     args = ap.parse_args()
 
     import torch
@@ -157,21 +158,10 @@ def main():
     total_cw = world * args.steps * B
     value = total_cw / elapsed
 
-    # ---- roofline: algorithmic bytes per decode launch / event-timed launch duration ----
+    # ---- roofline ---------------------------------------------------------------------------------------
     E = int(H.sum())  # nnz (SparseCode.sum() too)
-    s_b = 1 if args.algo in ("qminsum", "qms") else 4  # 5-bit mode s_m = s_L = 1 byte
-    bpc = algorithmic_bytes_per_cw(n, E, args.iters, s_b, s_b)
-    achieved = bpc * B / (gpu_ms * 1e-3) / 1e9
-    peak = 8000.0
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("code") == args.code and tj.get("batch") == B and tj.get("iters") == args.iters \
-                    and tj.get("algo") == args.algo and tj.get("path") == ("generic" if args.force_generic or not dec.qc_z else "qc"):
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    kpath = "generic-csr" if (args.force_generic or not dec.qc_z) else f"qc-z{dec.qc_z}"
+    roof = roofline(n, E, B, gpu_ms, args, kpath)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # CPU baseline at N=1 only
@@ -198,15 +188,9 @@ def main():
                 "clamp": args.clamp, "alpha": args.alpha, "early_stop": args.early_stop, "mod": args.mod,
                 "batch_per_gpu": B, "global_batch": B * world,
                 "parallelism": f"dp{world} (codeword shards, RCCL all-reduce of error counts only)",
-                "kernel_path": "generic-csr" if (args.force_generic or not dec.qc_z) else f"qc-z{dec.qc_z}",
+                "kernel_path": kpath,
             },
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                         "frac": achieved / peak, "traffic": traffic,
-                         "bytes_per_codeword_model": bpc, "launch_ms": gpu_ms,
-                         # measured HBM rate of the launch (PMC traffic / event time): the register/LDS-
-                         # resident QC kernels keep messages on chip, so frac > 1 on the survey's streaming
-                         # model while the bytes actually moved are the llr in / bits out
-                         "traffic_GBps": (traffic / (gpu_ms * 1e-3) / 1e9) if traffic else None},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "ber": {"ebn0_db": ebn0.tolist(), "coded_ber_info": coded_ber, "coded_bler": coded_bler,
                     "codewords_per_point": int(c[0, 2])},
@@ -214,6 +198,62 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# MI355X (MI355X_MICROARCH.md): 8 TB/s HBM3E; 256 CUs x 4 SIMD-32 at 2.4 GHz peak engine clock; a wave64 VALU
+# instruction takes 2 SIMD cycles; the LDS array of each CU runs one cycle per clock.
+HBM_PEAK_GBPS = 8000.0
+CLOCK_HZ = 2.4e9
+VALU_PEAK = 1024 * CLOCK_HZ / 2 / 1e9      # G wave64-VALU instructions / s
+LDS_PEAK = 256 * CLOCK_HZ / 1e9            # G LDS-array cycles / s (all CUs)
+
+
+def roofline(n, E, B, launch_ms, args, kpath):
+    """The decode launch against the resource that binds it.
+
+    * Streaming (generic CSR) kernels move every message through HBM each iteration: bound "hbm",
+      achieved = SURVEY §8(d) algorithmic bytes per launch / launch time.
+    * The register-resident QC kernels keep all messages on chip (HBM sees only llr in / bits out), so
+      HBM cannot bind them: bound = the busier of VALU issue and the LDS pipe (ds_bpermute lane
+      rotations), from the per-launch instruction / LDS-cycle counts that scripts/gpu_profile.sh measured
+      for this exact configuration (profiles/counters.json; deterministic for a fixed iteration count)
+      divided by this run's event-timed launch duration, against 2.4 GHz peak.  The survey's byte model
+      is kept beside it as hbm.model_frac (it exceeds 1 for on-chip kernels by construction) with the
+      measured PMC traffic.
+    """
+    s_b = 1 if args.algo in ("qminsum", "qms") else 4  # SURVEY §8(d): 5-bit mode s_m = s_L = 1 byte
+    bpc = algorithmic_bytes_per_cw(n, E, args.iters, s_b, s_b)
+    launch_s = launch_ms * 1e-3
+    model_gbps = bpc * B / launch_s / 1e9
+    rec = None
+    if os.path.exists(args.counters_json):
+        want = {"code": args.code, "algo": args.algo, "iters": args.iters, "early_stop": args.early_stop,
+                "batch_per_gpu": B, "kernel_path": kpath, "mod": args.mod}
+        for r in json.load(open(args.counters_json)):
+            if all(r["config"].get(k) == v for k, v in want.items()):
+                rec = r
+    c = rec["counters_per_launch"] if rec else {}
+    hbm_bytes = rec["derived"].get("hbm_bytes") if rec else None
+    hbm = {"model_bytes_per_codeword": bpc, "model_GBps": model_gbps, "model_frac": model_gbps / HBM_PEAK_GBPS,
+           "traffic_bytes_per_launch": hbm_bytes,
+           "traffic_GBps": hbm_bytes / launch_s / 1e9 if hbm_bytes else None,
+           "traffic_frac": hbm_bytes / launch_s / 1e9 / HBM_PEAK_GBPS if hbm_bytes else None}
+    out = {"launch_ms": launch_ms, "hbm": hbm,
+           "counters": (os.path.relpath(args.counters_json, ROOT) + f" [{rec['name']}]") if rec else None}
+    if kpath == "generic-csr" or "SQ_INSTS_VALU" not in c:
+        out.update(bound="hbm", achieved=model_gbps, peak=HBM_PEAK_GBPS, unit="GB/s",
+                   frac=model_gbps / HBM_PEAK_GBPS, traffic=hbm_bytes)
+        return out
+    valu = c["SQ_INSTS_VALU"] / launch_s / 1e9
+    lds = c.get("SQ_LDS_IDX_ACTIVE", 0.0) / launch_s / 1e9
+    out["valu"] = {"achieved": valu, "peak": VALU_PEAK, "unit": "G wave-instr/s", "frac": valu / VALU_PEAK,
+                   "insts_per_launch": c["SQ_INSTS_VALU"]}
+    out["lds"] = {"achieved": lds, "peak": LDS_PEAK, "unit": "G LDS-cycles/s", "frac": lds / LDS_PEAK,
+                  "cycles_per_launch": c.get("SQ_LDS_IDX_ACTIVE")}
+    b = "lds" if out["lds"]["frac"] > out["valu"]["frac"] else "valu"
+    out.update(bound=b, achieved=out[b]["achieved"], peak=out[b]["peak"], unit=out[b]["unit"], frac=out[b]["frac"],
+               traffic=hbm_bytes)
+    return out
 
 
 def cpu_baseline(H, args, rate):

@@ -12,7 +12,7 @@ data-path exchange, so scaling is weak).
 
 The other BASELINE.json configs are parity-test cases; their throughput lines (profiles/) come from
 the same script, e.g. configs[2]: --code wifi1944_56 --algo tanh --mod 16qam-ofdm --ebn0 4:0.5:9;
-configs[3]: --code wifi1296_23 --algo qminsum --iters 20 --early-stop; configs[4]: --code dvbs2s_12.
+configs[3]: --code wifi1296_23 --algo qminsum --iters 20 --early-stop; configs[4]: --code dvbs2_12 --batch 4096 (EN 302 307 rate-1/2 table).
 """
 import argparse
 import json
@@ -56,6 +56,9 @@ def main():
                     help="LLR generator (outside the timed region): BPSK/AWGN or the OFDM front end")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the decode_bits / tanh-SP side measurements")
+    ap.add_argument("--ref-cpu-json", default=os.path.join(ROOT, "profiles", "r02", "ref_cpu_wifi648.json"),
+                    help="the reference's own CPU decode_bits timing (scripts/time_reference_cpu.py)")
     ap.add_argument("--counters-json", default=os.path.join(ROOT, "profiles", "counters.json"),
                     help="per-launch PMC counts per configuration (scripts/gpu_profile.sh + counters_summary.py)")
     args = ap.parse_args()
@@ -166,6 +169,14 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # CPU baseline at N=1 only
         cpu = cpu_baseline(H, args, rate)
+    side = None
+    if rank == 0 and world == 1 and not args.no_dropin and B * n * 8 <= (1 << 32):
+        side = side_measurements(H, dec, llrs[len(ebn0) // 2], B, args)
+        ref = reference_cpu(args)
+        if cpu is not None and ref is not None:
+            ref["gpu_tanh_sp_over_reference"] = side["gpu_tanh_sp"]["cw_per_s"] / ref["value"]
+            ref["dropin_over_reference"] = side["dropin"]["cw_per_s"] / ref["value"]
+            cpu["reference"] = ref
 
     if rank == 0:
         out = {
@@ -192,6 +203,8 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
+            "dropin_cw_per_s": side["dropin"]["cw_per_s"] if side else None,
+            "side": side,
             "ber": {"ebn0_db": ebn0.tolist(), "coded_ber_info": coded_ber, "coded_bler": coded_bler,
                     "codewords_per_point": int(c[0, 2])},
         }
@@ -254,6 +267,62 @@ def roofline(n, E, B, launch_ms, args, kpath):
     out.update(bound=b, achieved=out[b]["achieved"], peak=out[b]["peak"], unit=out[b]["unit"], frac=out[b]["frac"],
                traffic=hbm_bytes)
     return out
+
+
+def side_measurements(H, dec, llr_dev, B, args):
+    """Two secondary numbers next to the headline (never `value`):
+    * ``dropin``: the reference's boundary itself, ``decode_bits(llrs_f64, H, iters, 256, 10)``
+      (ofdm_functions.py:131-163) from host float64 LLRs to host float64 bits — PCIe, staging and the
+      f64<->f32 conversions included (ldpc_decode_bits_host's pinned two-stream pipeline);
+    * ``gpu_tanh_sp``: the reference's algorithm (tanh sum-product, 50 it, clamp 10) on the same H with
+      LLRs resident in HBM — the apples-to-apples partner of the reference CPU number."""
+    import torch
+    import ldpc_amd
+    from ldpc_amd import _abi
+    lib = _abi.load()
+    host = llr_dev.double().cpu().numpy()
+    ldpc_amd.decode_bits(host[:512], H, args.iters, 256, 10.0)   # graph + staging ring allocation
+    t = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        out = ldpc_amd.decode_bits(host, H, args.iters, 256, 10.0)
+    dt = (time.perf_counter() - t) / reps
+    dropin = {"cw_per_s": B / dt, "seconds": dt, "codewords": B, "iters": args.iters, "algo": "tanh",
+              "clamp": 10.0, "batch_size": 256, "bits_set": int(out.sum()),
+              "what": "decode_bits(llrs float64 host, H, iters, 256, 10) end to end: f64->f32 staging, "
+                      "H2D, decode, D2H, 0/1 float64 expansion"}
+    p = dec.params(args.iters, "tanh", 10.0, device_ptrs=True)
+    wsb = dec.workspace_bytes(B, p)
+    ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=llr_dev.device)
+    bits = torch.empty((B, dec.n), dtype=torch.uint8, device=llr_dev.device)
+    st = torch.cuda.current_stream().cuda_stream
+    run = lambda: _abi.check(lib.ldpc_decode_ex(dec._h, llr_dev.data_ptr(), B, p, bits.data_ptr(), None, None,
+                                                ws.data_ptr(), wsb, st))
+    run()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    steps = 3
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / steps
+    return {"dropin": dropin,
+            "gpu_tanh_sp": {"cw_per_s": B / dt, "ms_per_launch": dt * 1e3, "codewords": B, "iters": args.iters,
+                            "clamp": 10.0, "what": "tanh sum-product (the reference's algorithm), LLRs in HBM"}}
+
+
+def reference_cpu(args):
+    """The reference's own CPU path, timed in the build container by scripts/time_reference_cpu.py (the
+    reference cannot travel to the GPU box); carried here with its provenance."""
+    if args.code != "wifi648_12" or not os.path.exists(args.ref_cpu_json):
+        return None
+    r = json.load(open(args.ref_cpu_json))
+    return {"value": r["reference_cw_per_s"], "unit": "codewords/s", "cores": r["threads"], "kind": "reference",
+            "sample": f"{r['codewords']} codewords, decode_bits(llrs, H, {r['iters']}, {r['batch_size']}, "
+                      f"{r['clamp']:g}) tanh-SP on the real (648,1/2) H at Eb/N0 {r['ebn0_db']} dB, "
+                      f"{r['reference_seconds']:.1f} s, torch {r['torch']} CPU, {r['threads']} threads",
+            "where": "build container (8-core Xeon, no GPU): " + os.path.relpath(args.ref_cpu_json, ROOT),
+            "algo": "tanh", "iters": r["iters"]}
 
 
 def cpu_baseline(H, args, rate):

@@ -120,6 +120,27 @@ int ldpc_decode_weighted(const ldpc_graph* g, const void* llr, int64_t B, const 
                          const ldpc_bp_weights* w, uint8_t* bits_out, void* soft_out, int32_t* iters_used,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+/* BeliefPropagation.forward(x, llr, clamp) with NON-ZERO initial messages x (pytorch/bp/bp.py:43-47: the
+ * first layer consumes x exactly as later layers consume the previous c2v).  x0: DEVICE [B][E] in the
+ * reference's check-order edge numbering (masking.py:84-88), element type = the decode precision; NULL =
+ * zeros.  w: optional weights as ldpc_decode_weighted (NULL = plain BP).  Requires LDPC_F_DEVICE_PTRS when
+ * x0 is given; tanh sum-product without early stop; generic CSR kernels (workspace as LDPC_F_FORCE_GENERIC). */
+int ldpc_decode_x0(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_params* p, const ldpc_bp_weights* w,
+                   const void* x0, uint8_t* bits_out, void* soft_out, int32_t* iters_used, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+/* The drop-in decode_bits (pytorch/ofdm/ofdm_functions.py:131-163) end to end from HOST memory: rows
+ * codewords of float64 llr[rows][n] (log P1/P0) -> out[rows][n] float64 0.0/1.0 (np.round(p1) semantics).
+ * The caller passes rows = (N // batch_size) * batch_size and leaves the remainder rows zero, as the
+ * reference does (:133-135); every batch is independent, so the batches are decoded in chunks of `chunk`
+ * codewords (0 = ~16 MB of float32 LLRs) through a two-slot pinned staging ring: the host converts chunk
+ * c+1 to float32 (the reference's torch.tensor(..., dtype=torch.float), :156) while the GPU copies in,
+ * decodes and copies out chunk c on its own stream, and the host expands chunk c-1's uint8 bits to float64.
+ * `threads` host threads for the staging copies (0 = min(16, hardware threads)).  p: float32 arithmetic on
+ * host buffers (LDPC_F_F64 / LDPC_F_DEVICE_PTRS / LDPC_F_SOFT_Z are EINVAL); synchronous. */
+int ldpc_decode_bits_host(const ldpc_graph* g, const double* llr, int64_t rows, const ldpc_params* p, double* out,
+                          int64_t chunk, int32_t threads);
+
 /* Error counting on device, the metrics of evaluate_quantized.py:139-141 for one SNR point:
  *   counts[0] += bit errors over the first info_bits positions of each codeword (coded BER numerator)
  *   counts[1] += codewords with any error over all n positions              (coded BLER numerator)

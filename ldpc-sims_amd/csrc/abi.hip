@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -24,6 +25,19 @@ struct ldpc_graph {
     std::mutex mtx;  // guards the internal workspace
     void* ws = nullptr;
     size_t ws_bytes = 0;
+    // ldpc_decode_bits_host's staging ring (allocated on first use, reused; guarded by pipe_mtx)
+    std::mutex pipe_mtx;
+    struct Pipe {
+        int64_t chunk = 0;        // codewords per slot
+        size_t ws_bytes = 0;      // decode workspace per slot
+        float* h_llr[2] = {};     // pinned host: float32 llr of one chunk
+        uint8_t* h_bits[2] = {};  // pinned host: hard bits of one chunk
+        float* d_llr[2] = {};
+        uint8_t* d_bits[2] = {};
+        void* d_ws[2] = {};
+        hipStream_t st[2] = {};
+        hipEvent_t done[2] = {};
+    } pipe;
 };
 
 namespace ldpc {
@@ -247,6 +261,62 @@ static const QCSpec* detect_qc(int m, int n, const std::vector<int32_t>& row_ptr
     return nullptr;
 }
 
+// ---- staging ring of ldpc_decode_bits_host --------------------------------------------------------
+static void pipe_free(ldpc_graph* g) {
+    auto& P = g->pipe;
+    for (int i = 0; i < 2; ++i) {
+        if (P.done[i]) (void)hipEventDestroy(P.done[i]);
+        if (P.st[i]) (void)hipStreamDestroy(P.st[i]);
+        if (P.h_llr[i]) (void)hipHostFree(P.h_llr[i]);
+        if (P.h_bits[i]) (void)hipHostFree(P.h_bits[i]);
+        if (P.d_llr[i]) (void)hipFree(P.d_llr[i]);
+        if (P.d_bits[i]) (void)hipFree(P.d_bits[i]);
+        if (P.d_ws[i]) (void)hipFree(P.d_ws[i]);
+    }
+    P = ldpc_graph::Pipe{};
+}
+
+static int pipe_alloc(ldpc_graph* g, int64_t chunk, size_t ws_bytes) {
+    auto& P = g->pipe;
+    if (P.chunk >= chunk && P.ws_bytes >= ws_bytes) return LDPC_OK;
+    pipe_free(g);
+    const size_t nl = (size_t)chunk * g->n;
+    for (int i = 0; i < 2; ++i) {
+        hipError_t e = hipHostMalloc((void**)&P.h_llr[i], nl * 4, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&P.h_bits[i], nl, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc((void**)&P.d_llr[i], nl * 4);
+        if (e == hipSuccess) e = hipMalloc((void**)&P.d_bits[i], nl);
+        if (e == hipSuccess) e = hipMalloc(&P.d_ws[i], ws_bytes);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&P.st[i], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&P.done[i], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            pipe_free(g);
+            return set_error(LDPC_ENOMEM, "decode_bits staging (%lld codewords): %s", (long long)chunk, hipGetErrorString(e));
+        }
+    }
+    P.chunk = chunk;
+    P.ws_bytes = ws_bytes;
+    return LDPC_OK;
+}
+
+// Host-side work of one chunk split over worker threads (the staging copies are memory-bound).
+template <class F>
+static void parallel_rows(int64_t rows, int threads, F&& f) {
+    if (threads <= 1 || rows < 2 * threads) {
+        f((int64_t)0, rows);
+        return;
+    }
+    std::vector<std::thread> ts;
+    ts.reserve(threads - 1);
+    const int64_t per = (rows + threads - 1) / threads;
+    for (int t = 1; t < threads; ++t) {
+        const int64_t a = t * per, b = std::min(rows, a + per);
+        if (a < b) ts.emplace_back([&f, a, b] { f(a, b); });
+    }
+    f((int64_t)0, std::min(rows, per));
+    for (auto& t : ts) t.join();
+}
+
 }  // namespace ldpc
 
 using namespace ldpc;
@@ -315,6 +385,7 @@ int ldpc_graph_destroy(ldpc_graph* g) {
     (void)hipFree(g->d_var_edges);
     (void)hipFree(g->d_wofs);
     if (g->ws) (void)hipFree(g->ws);
+    pipe_free(g);
     delete g;
     return LDPC_OK;
 }
@@ -429,6 +500,20 @@ int ldpc_decode_weighted(const ldpc_graph* g, const void* llr, int64_t B, const 
     return decode_impl(g, llr, B, &q, bits_out, soft_out, iters_used, workspace, workspace_bytes, stream, &bw);
 }
 
+int ldpc_decode_x0(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_params* p, const ldpc_bp_weights* w,
+                   const void* x0, uint8_t* bits_out, void* soft_out, int32_t* iters_used, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+    if (!p || !params_valid(p)) return set_error(LDPC_EINVAL, "invalid ldpc_params");
+    if (p->algo != LDPC_ALGO_TANH_SP || (p->flags & LDPC_F_EARLY_STOP))
+        return set_error(LDPC_EUNSUPPORTED, "initial messages: tanh sum-product without early stop");
+    if (x0 && !(p->flags & LDPC_F_DEVICE_PTRS)) return set_error(LDPC_EINVAL, "x0 needs LDPC_F_DEVICE_PTRS");
+    ldpc_params q = *p;
+    q.flags |= LDPC_F_FORCE_GENERIC;
+    BPWeights bw{w ? w->vn : nullptr, w ? w->llr : nullptr, w ? w->fin : nullptr, w ? w->fin_llr : nullptr};
+    bw.c2v0 = x0;
+    return decode_impl(g, llr, B, &q, bits_out, soft_out, iters_used, workspace, workspace_bytes, stream, &bw);
+}
+
 int ldpc_decode(const ldpc_graph* g, const float* llr, int64_t B, int32_t iters, float clamp, int32_t algo,
                 int32_t flags, uint8_t* bits_out, float* soft_out, void* stream) {
     ldpc_params p{};
@@ -442,6 +527,73 @@ int ldpc_decode(const ldpc_graph* g, const float* llr, int64_t B, int32_t iters,
     p.app_max = 127;
     p.qstep = 1.0f;
     return ldpc_decode_ex(g, llr, B, &p, bits_out, soft_out, nullptr, nullptr, 0, stream);
+}
+
+int ldpc_decode_bits_host(const ldpc_graph* gc, const double* llr, int64_t rows, const ldpc_params* p, double* out,
+                          int64_t chunk, int32_t threads) {
+    ldpc_graph* g = const_cast<ldpc_graph*>(gc);
+    if (!g || !p || rows < 0 || (rows > 0 && (!llr || !out))) return set_error(LDPC_EINVAL, "bad decode_bits arguments");
+    if (!params_valid(p)) return set_error(LDPC_EINVAL, "invalid ldpc_params");
+    if (p->flags & (LDPC_F_F64 | LDPC_F_DEVICE_PTRS | LDPC_F_SOFT_Z))
+        return set_error(LDPC_EINVAL, "decode_bits_host: float32 arithmetic on host buffers, bits only");
+    if (rows == 0) return LDPC_OK;
+    const int n = g->n;
+    if (chunk <= 0) chunk = std::max<int64_t>(256, ((int64_t)16 << 20) / ((int64_t)n * 4) / 256 * 256);  // ~16 MB of f32
+    chunk = std::min(chunk, rows);
+    if (threads <= 0) threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    ldpc_params q = *p;
+    q.flags |= LDPC_F_DEVICE_PTRS;
+    DeviceGuard dg(g->device);
+    std::lock_guard<std::mutex> lock(g->pipe_mtx);
+    int rc = pipe_alloc(g, chunk, std::max<size_t>(256, kernel_ws(g, chunk, &q)));
+    if (rc != LDPC_OK) return rc;
+    auto& P = g->pipe;
+    hipError_t e;
+    for (int i = 0; i < 2; ++i)  // a previous call that failed midway may still have copies in flight
+        if ((e = hipStreamSynchronize(P.st[i])) != hipSuccess)
+            return set_error(LDPC_EHIP, "decode_bits: %s", hipGetErrorString(e));
+    const int64_t nchunks = (rows + chunk - 1) / chunk;
+    // drain(slot, c): chunk c's bits have landed in h_bits[slot]: expand them to 0.0/1.0 doubles in `out`
+    auto drain = [&](int slot, int64_t c) -> int {
+        if ((e = hipEventSynchronize(P.done[slot])) != hipSuccess)
+            return set_error(LDPC_EHIP, "decode_bits chunk %lld: %s", (long long)c, hipGetErrorString(e));
+        const int64_t r0 = c * chunk, nr = std::min(chunk, rows - r0);
+        const uint8_t* hb = P.h_bits[slot];
+        parallel_rows(nr, threads, [&](int64_t a, int64_t b) {
+            const uint8_t* s = hb + a * n;
+            double* d = out + (r0 + a) * n;
+            for (int64_t i = 0, cnt = (b - a) * n; i < cnt; ++i) d[i] = (double)s[i];
+        });
+        return LDPC_OK;
+    };
+    // Two slots: while the GPU copies in / decodes / copies out chunk c on stream st[c&1], the host drains
+    // chunk c-2 and converts chunk c+1 into the other slot; the float64 -> float32 conversion (the
+    // reference's torch.tensor(..., dtype=torch.float), ofdm_functions.py:156) is fused into the staging
+    // copy, so PCIe carries 4 B per LLR in and 1 B per bit out.
+    for (int64_t c = 0; c < nchunks; ++c) {
+        const int slot = (int)(c & 1);
+        if (c >= 2 && (rc = drain(slot, c - 2)) != LDPC_OK) return rc;
+        const int64_t r0 = c * chunk, nr = std::min(chunk, rows - r0);
+        float* hl = P.h_llr[slot];
+        parallel_rows(nr, threads, [&](int64_t a, int64_t b) {
+            const double* s = llr + (r0 + a) * n;
+            float* d = hl + a * n;
+            for (int64_t i = 0, cnt = (b - a) * n; i < cnt; ++i) d[i] = (float)s[i];
+        });
+        hipStream_t st = P.st[slot];
+        if ((e = hipMemcpyAsync(P.d_llr[slot], hl, (size_t)nr * n * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return set_error(LDPC_EHIP, "decode_bits H2D: %s", hipGetErrorString(e));
+        rc = decode_impl(g, P.d_llr[slot], nr, &q, P.d_bits[slot], nullptr, nullptr, P.d_ws[slot], P.ws_bytes, st,
+                         nullptr);
+        if (rc != LDPC_OK) return rc;
+        if ((e = hipMemcpyAsync(P.h_bits[slot], P.d_bits[slot], (size_t)nr * n, hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return set_error(LDPC_EHIP, "decode_bits D2H: %s", hipGetErrorString(e));
+        if ((e = hipEventRecord(P.done[slot], st)) != hipSuccess)
+            return set_error(LDPC_EHIP, "decode_bits event: %s", hipGetErrorString(e));
+    }
+    for (int64_t c = std::max<int64_t>(0, nchunks - 2); c < nchunks; ++c)
+        if ((rc = drain((int)(c & 1), c)) != LDPC_OK) return rc;
+    return LDPC_OK;
 }
 
 int ldpc_count_errors(const uint8_t* bits, const uint8_t* ref, int64_t B, int32_t n, int32_t info_bits, int64_t* counts,

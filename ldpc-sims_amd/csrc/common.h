@@ -152,6 +152,7 @@ struct GenericArgs {
 // null (= all ones).  vn [iters][W], lw [iters][n], fin [E] (var-slot order), flw [n].
 struct BPWeights {
     const void *vn, *lw, *fin, *flw;
+    const void* c2v0 = nullptr;  // initial c2v [B][E] check-order (the reference's x, bp/bp.py:43-47); NULL = 0
 };
 size_t generic_workspace(const GenericArgs& g, int64_t B, const ldpc_params& p);
 int generic_decode(const GenericArgs& g, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits,

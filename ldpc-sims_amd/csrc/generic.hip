@@ -31,9 +31,14 @@ int generic_decode(const GenericArgs& g, const void* llr_dev, int64_t B, const l
     for (int64_t o = 0; o < B; o += bc) {
         const int64_t b = (B - o < bc) ? B - o : bc;
         const int64_t vo = o * g.n;
+        BPWeights wc{};
+        if (w) {
+            wc = *w;
+            if (w->c2v0) wc.c2v0 = (const char*)w->c2v0 + o * (int64_t)g.E * (int64_t)elem;
+        }
         const int rc = decode_chunk(g, (const char*)llr_dev + vo * elem, b, p, bits ? bits + vo : nullptr,
                                     soft ? (void*)((char*)soft + vo * elem) : nullptr, iters_used ? iters_used + o : nullptr,
-                                    ws, st, w);
+                                    ws, st, w ? &wc : nullptr);
         if (rc != LDPC_OK) return rc;
     }
     return LDPC_OK;
@@ -43,7 +48,7 @@ static int decode_chunk(const GenericArgs& g, const void* llr_dev, int64_t B, co
                         void* soft, int32_t* iters_used, char* ws, hipStream_t st, const BPWeights* w) {
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
     if (w && (p.algo != LDPC_ALGO_TANH_SP || es))
-        return set_error(LDPC_EUNSUPPORTED, "weighted BP is tanh sum-product without early stop");
+        return set_error(LDPC_EUNSUPPORTED, "weighted BP / initial messages: tanh sum-product without early stop");
     int rc;
     if (p.algo == LDPC_ALGO_TANH_SP) {
         if (p.flags & LDPC_F_F64) {

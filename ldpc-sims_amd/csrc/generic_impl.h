@@ -28,7 +28,9 @@ namespace ldpc {
 
 constexpr int kTB = 256;
 
-template <typename T>
+// [B][n] row-major -> [n][ldb] edge-major (negated for the LLR: the reference decodes -llr, bp.py:47; as is
+// for initial c2v messages, n = E)
+template <typename T, bool NEG = true>
 __global__ __launch_bounds__(256) void k_load_llr(const T* __restrict__ llr, T* __restrict__ L, int64_t B, int n,
                                                   int64_t ldb) {
     __shared__ T tile[64][65];
@@ -38,7 +40,7 @@ __global__ __launch_bounds__(256) void k_load_llr(const T* __restrict__ llr, T* 
     for (int r = ty; r < 64; r += 4) {
         const int64_t cw = cw0 + r;
         const int v = v0 + tx;
-        if (cw < B && v < n) tile[r][tx] = -llr[cw * n + v];
+        if (cw < B && v < n) tile[r][tx] = NEG ? -llr[cw * n + v] : llr[cw * n + v];
     }
     __syncthreads();
     for (int r = ty; r < 64; r += 4) {
@@ -537,6 +539,9 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     const dim3 tb(kTB);
     const unsigned gcw = (unsigned)((B + kTB - 1) / kTB);
     k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb);
+    // non-zero initial messages x (bp/bp.py:43-47): iteration 0 reads them like any later iteration
+    const T* x0 = wts ? (const T*)wts->c2v0 : nullptr;
+    if (x0) k_load_llr<T, false><<<dim3((unsigned)((B + 63) / 64), (g.E + 63) / 64), tb, 0, st>>>(x0, c2v, B, g.E, ldb);
     if (ES) {
         if (hipMemsetAsync(done, 0, (size_t)ldb, st) != hipSuccess || hipMemsetAsync(unsat, 0, (size_t)ldb, st) != hipSuccess)
             return set_error(LDPC_EHIP, "early-stop state init failed");
@@ -557,8 +562,8 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
                     (unsigned)((nodes + (256 >> tpl2) - 1) / (256 >> tpl2)));
     };
     for (int it = 0; it < p.iters; ++it) {
-        const int first = (it == 0);
-        if (!MS && wts) {
+        const int first = (it == 0) && !x0;
+        if (!MS && wts && (wts->vn || wts->lw)) {
             const T* vn_it = w_vn ? w_vn + (int64_t)it * g.W : nullptr;
             const T* lw_it = w_lw ? w_lw + (int64_t)it * g.n : nullptr;
 #define VNW1(D, VV) \
@@ -615,7 +620,7 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
 #undef CN
 #undef CN1
     }
-    if (p.iters == 0) (void)hipMemsetAsync(c2v, 0, sizeof(T) * (size_t)g.E * ldb, st);
+    if (p.iters == 0 && !x0) (void)hipMemsetAsync(c2v, 0, sizeof(T) * (size_t)g.E * ldb, st);
     k_final<T, 32, MS><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(g.var_ptr, g.var_edges, L, c2v, B,
                                                                                       ldb, g.n, bits, soft, soft_z,
                                                                                       wts ? (const T*)wts->fin : nullptr,

@@ -21,7 +21,7 @@ EXPORTS = (
     "ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
     "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
     "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_adc_quantize", "ldpc_weights_layout",
-    "ldpc_decode_weighted", "ldpc_last_error", "ldpc_device_count",
+    "ldpc_decode_weighted", "ldpc_decode_x0", "ldpc_decode_bits_host", "ldpc_last_error", "ldpc_device_count",
     "ldpc_version",
 )
 
@@ -84,10 +84,13 @@ def load(path: str | None = None):
     L.ldpc_weights_layout.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     L.ldpc_decode_weighted.argtypes = [vp, vp, i64, ctypes.POINTER(Params), ctypes.POINTER(BPWeights), vp, vp, vp,
                                        vp, sz, vp]
+    L.ldpc_decode_x0.argtypes = [vp, vp, i64, ctypes.POINTER(Params), ctypes.POINTER(BPWeights), vp, vp, vp, vp,
+                                 vp, sz, vp]
+    L.ldpc_decode_bits_host.argtypes = [vp, vp, i64, ctypes.POINTER(Params), vp, i64, i32]
     for f in ("ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
               "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
               "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_adc_quantize", "ldpc_weights_layout", "ldpc_decode_weighted",
-              "ldpc_device_count"):
+              "ldpc_decode_x0", "ldpc_decode_bits_host", "ldpc_device_count"):
         getattr(L, f).restype = ctypes.c_int
     L.ldpc_last_error.restype = ctypes.c_char_p
     L.ldpc_version.restype = ctypes.c_char_p

@@ -107,23 +107,33 @@ class Decoder:
 
     def decode(self, llr, iters: int, *, algo="tanh", clamp=10.0, alpha=1.0, beta=0.0, early_stop=False,
                precision="f32", soft=None, qmax=15, app_max=127, qstep=1.0, force_generic=False, stream=None,
-               want_bits=True, want_iters=False, weights=None):
+               want_bits=True, want_iters=False, weights=None, x0=None):
         """Decode a (B, n) batch of LLRs (log P1/P0).  numpy in -> numpy out (host staging inside the
         library); torch GPU tensor in (on this decoder's device) -> torch GPU tensors out, asynchronous on
         ``stream`` (a ``torch.cuda.Stream``; default: the current stream; a side stream first waits for the
         current one, and the outputs are allocated on and ordered by the side stream) with a
         torch-allocated workspace.  Returns dict(bits, soft, iters_used).
-        ``weights``: weighted BP (tanh-SP only), compact layout of ``Graph.compact_weights``."""
+        ``weights``: weighted BP (tanh-SP only), compact layout of ``Graph.compact_weights``.
+        ``x0``: initial c2v messages (B, E) in check-order — the reference's ``x`` (``bp/bp.py:43-47``);
+        torch GPU tensors only (tanh-SP, no early stop, generic kernels)."""
         is_torch = type(llr).__module__.startswith("torch")
         on_gpu = is_torch and llr.is_cuda
         fdt = np.float64 if precision == "f64" else np.float32
-        if weights is not None:
+        if weights is not None or x0 is not None:
             force_generic = True
+        if x0 is not None and not on_gpu:
+            raise ValueError("x0 (initial messages) needs torch GPU tensors for llr and x0")
         p = self.params(iters, algo, clamp, alpha, beta, early_stop, precision, soft or "p1", qmax, app_max,
                         qstep, force_generic, device_ptrs=on_gpu)
         wstruct, _wkeep = (self.device_weights(weights, iters, precision) if weights is not None else (None, None))
 
+        x0t = None
+
         def call(*args):
+            if x0t is not None:
+                return self.lib.ldpc_decode_x0(self._h, args[0], args[1], ctypes.byref(p),
+                                               ctypes.byref(wstruct) if wstruct is not None else None,
+                                               x0t.data_ptr(), *args[2:])
             if wstruct is None:
                 return self.lib.ldpc_decode_ex(self._h, args[0], args[1], ctypes.byref(p), *args[2:])
             return self.lib.ldpc_decode_weighted(self._h, args[0], args[1], ctypes.byref(p), ctypes.byref(wstruct),
@@ -148,6 +158,12 @@ class Decoder:
                     raise RuntimeError(f"llr must be (B, {self.n}), got {tuple(x.shape)}")
                 B = x.shape[0]
                 dev = x.device
+                if x0 is not None:
+                    if x0.device != llr.device:
+                        raise ValueError(f"x0 is on {x0.device}, llr on {llr.device}")
+                    x0t = x0.detach().to(tdt).contiguous()
+                    if tuple(x0t.shape) != (B, self.E):
+                        raise RuntimeError(f"x0 must be (B, E) = ({B}, {self.E}), got {tuple(x0t.shape)}")
                 bits = torch.empty((B, self.n), dtype=torch.uint8, device=dev) if want_bits else None
                 sft = torch.empty((B, self.n), dtype=tdt, device=dev) if soft else None
                 used = torch.empty((B,), dtype=torch.int32, device=dev) if want_iters else None
@@ -233,11 +249,12 @@ def decode_bits(llrs, H, bp_iterations, batch_size, clamp_value):
     if llrs.ndim != 2 or llrs.shape[1] != hshape[1]:
         raise RuntimeError(f"llrs shape {llrs.shape} does not match H {hshape}")
     dec = get_decoder(H)
-    chunk = max(batch_size, (1 << 26) // max(dec.E, 1) // batch_size * batch_size)
-    for s in range(0, rows, chunk):
-        e = min(rows, s + chunk)
-        r = dec.decode(llrs[s:e].astype(np.float32), int(bp_iterations), algo="tanh", clamp=float(clamp_value))
-        output_bits[s:e] = r["bits"]
+    x = np.ascontiguousarray(llrs, dtype=np.float64)
+    p = dec.params(int(bp_iterations), "tanh", float(clamp_value))
+    # float64 -> float32 staging, chunked H2D / decode / D2H on two streams and the 0/1 float64 expansion
+    # all run inside the library (ldpc_decode_bits_host); rows past `rows` stay 0 as in the reference
+    check(dec.lib.ldpc_decode_bits_host(dec._h, x.ctypes.data, rows, ctypes.byref(p), output_bits.ctypes.data,
+                                        0, 0))
     return output_bits
 
 
@@ -251,8 +268,8 @@ def _make_bp_module():
     class BeliefPropagation(nn.Module):
         """``bp/bp.py:19-62`` interface: ``BeliefPropagation(H, iterations)``, ``forward(x, llr, clamp)``
         returns ``p1 = 1 - sigmoid(z)`` (B, n); ``.double()`` switches to float64 arithmetic like the
-        reference module; ``layer_size()`` = number of edges E.  ``x`` (initial c2v messages, check-order)
-        must be zero, which is what every reference caller passes (``ofdm_functions.py:157``).
+        reference module; ``layer_size()`` = number of edges E.  ``x`` = initial c2v messages in check-order
+        (every reference caller passes zeros, ``ofdm_functions.py:157``; non-zero x runs ldpc_decode_x0).
 
         Weighted ("neural") BP forward: ``set_weights(...)`` with the reference's dense per-layer
         ``input_weight`` / ``llr_weight`` tensors, or ``load_reference_state_dict(sd)`` with a reference
@@ -297,13 +314,16 @@ def _make_bp_module():
                                     sd.get("final_layer.0.input_weight"), sd.get("final_layer.0.llr_weight"))
 
         def forward(self, x, llr, clamp_value):
-            if x is not None and bool(torch.count_nonzero(x)):
-                raise NotImplementedError("non-zero initial messages x are not supported")
             precision = "f64" if self._dtype_probe.dtype == torch.float64 else "f32"
             dev = llr.device.index if llr.is_cuda else (torch.cuda.current_device() if torch.cuda.is_available() else 0)
             d = get_decoder(self.H, dev or 0)
+            x0 = x if (x is not None and bool(torch.count_nonzero(x))) else None
+            if x0 is not None and not llr.is_cuda:
+                # non-zero initial messages go through the device path: stage both to the GPU and back
+                p1 = self.forward(x.to(f"cuda:{dev or 0}"), llr.to(f"cuda:{dev or 0}"), clamp_value)
+                return p1.cpu()
             r = d.decode(llr, self.iterations, algo="tanh", clamp=float(clamp_value), precision=precision,
-                         soft="p1", want_bits=False, weights=self.weights)
+                         soft="p1", want_bits=False, weights=self.weights, x0=x0)
             p1 = r["soft"]
             if not llr.is_cuda:
                 p1 = torch.from_numpy(p1)

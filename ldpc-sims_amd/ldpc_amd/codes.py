@@ -144,13 +144,15 @@ def wifi_code(n: int, rate: str) -> QCCode:
 
 
 def available_codes():
-    return ["peg64_32"] + [f"wifi{n}_{r.replace('/', '')}" for (n, r) in sorted(_WIFI_TABLES)] + ["dvbs2s_12"]
+    return ["peg64_32"] + [f"wifi{n}_{r.replace('/', '')}" for (n, r) in sorted(_WIFI_TABLES)] + ["dvbs2_12", "dvbs2s_12"]
 
 
 def get_code(name: str):
     """Return ``(H, qc)`` for a named code; ``qc`` is the QCCode or ``None``."""
     if name == "peg64_32":
         return peg_64_32(), None
+    if name == "dvbs2_12":
+        return dvbs2_12(), None
     if name == "dvbs2s_12":
         return dvbs2_shaped(), None
     if name.startswith("wifi"):
@@ -377,21 +379,148 @@ class SparseCode:
         return H
 
 
-def dvbs2_shaped(seed: int = 2019) -> SparseCode:
-    """A DVB-S2-SHAPED normal-frame rate-1/2 IRA code: n = 64800, k = 32400, q = 90, 90 address rows
-    (36 of degree 8, 54 of degree 3), staircase accumulator parity — exactly the structure, degree
-    profile and edge count (E = 226,799) of EN 302 307 Table B.5, but with seeded pseudo-random
-    addresses: the standard's address table is not available offline.  Parity of the table contents is
-    therefore UNPINNED; the decoder does not care (it is the generic CSR path).
-
-    Info bit i of group g connects to checks (x + (i mod 360) * q) mod m for every address x of row g.
-    Each residue class mod q receives exactly 5 addresses, so every check has 5 info edges + 2 parity
-    edges (check 0: 1 parity edge), as in the standard."""
-    n, k, q, Z = 64800, 32400, 90, 360
+def _ira_code(groups, name: str, n: int = 64800, k: int = 32400, q: int = 90, Z: int = 360) -> SparseCode:
+    """IRA code of EN 302 307 §5.3.2: information bit i of group g (i = 0..Z-1) is accumulated into parity
+    address (x + i*q) mod m for every address x of row g; parity bit c of check c chains with c-1
+    (staircase, p_c ^= p_{c-1}).  Returns the check-major CSR with ascending columns."""
     m = n - k
+    cols, chks = [], []
+    i = np.arange(Z)
+    for g, xs in enumerate(groups):
+        for x in xs:
+            chks.append((int(x) + i * q) % m)
+            cols.append(g * Z + i)
+    c = np.arange(m)
+    chks += [c, c[1:]]
+    cols += [k + c, k + c[1:] - 1]
+    chks = np.concatenate(chks)
+    cols = np.concatenate(cols)
+    order = np.lexsort((cols, chks))
+    chks, cols = chks[order], cols[order]
+    row_ptr = np.zeros(m + 1, np.int64)
+    np.add.at(row_ptr, chks + 1, 1)
+    row_ptr = np.cumsum(row_ptr).astype(np.int32)
+    dmax = max(len(g) for g in groups)
+    return SparseCode(m, n, row_ptr, cols.astype(np.int32), name=name,
+                      info_groups=np.array([np.pad(np.asarray(g), (0, dmax - len(g)), constant_values=-1)
+                                            for g in groups]))
+
+
+# EN 302 307 (DVB-S2) Annex B, normal frame (n = 64800), rate 1/2: one row of parity-bit accumulator
+# addresses per group of 360 information bits; 36 rows of degree 8, then 54 of degree 3.  Typed from the
+# standard.  Structural checks (tests/test_codes.py::test_dvbs2_table_structure): every residue mod 90
+# appears exactly 5 times (every check: 5 info edges + 2 staircase edges), no repeated edge, girth >= 6
+# (no 4-cycle), IRA-encoded codewords have zero syndrome.  The reference cannot instantiate a code this
+# size (masking.py:36-38 builds dense E x E masks), so decoding parity on it is UNPINNED against the
+# reference; it is pinned against the oracle (bit-exact) like every other code.
+_DVBS2_N_12 = """54 9318 14392 27561 26909 10219 2534 8597
+55 7263 4635 2530 28130 3033 23830 3651
+56 24731 23583 26036 17299 5750 792 9169
+57 5811 26154 18653 11551 15447 13685 16264
+58 12610 11347 28768 2792 3174 29371 12997
+59 16789 16018 21449 6165 21202 15850 3186
+60 31016 21449 17618 6213 12166 8334 18212
+61 22836 14213 11327 5896 718 11727 9308
+62 2091 24941 29966 23634 9013 15587 5444
+63 22207 3983 16904 28534 21415 27524 25912
+64 25687 4501 22193 14665 14798 16158 5491
+65 4520 17094 23397 4264 22370 16941 21526
+66 10490 6182 32370 9597 30841 25954 2762
+67 22120 22865 29870 15147 13668 14955 19235
+68 6689 18408 18346 9918 25746 5443 20645
+69 29982 12529 13858 4746 30370 10023 24828
+70 1262 28032 29888 13063 24033 21951 7863
+71 6594 29642 31451 14831 9509 9335 31552
+72 1358 6454 16633 20354 24598 624 5265
+73 19529 295 18011 3080 13364 8032 15323
+74 11981 1510 7960 21462 9129 11370 25741
+75 9276 29656 4543 30699 20646 21921 28050
+76 15975 25634 5520 31119 13715 21949 19605
+77 18688 4608 31755 30165 13103 10706 29224
+78 21514 23117 12245 26035 31656 25631 30699
+79 9674 24966 31285 29908 17042 24588 31857
+80 21856 27777 29919 27000 14897 11409 7122
+81 29773 23310 263 4877 28622 20545 22092
+82 15605 5651 21864 3967 14419 22757 15896
+83 30145 1759 10139 29223 26086 10556 5098
+84 18815 16575 2936 24457 26738 6030 505
+85 30326 22298 27562 20131 26390 6247 24791
+86 928 29246 21246 12400 15311 32309 18608
+87 20314 6025 26689 16302 2296 3244 19613
+88 6237 11943 22851 15642 23857 15112 20947
+89 26403 25168 19038 18384 8882 12719 7093
+0 14567 24965
+1 3908 100
+2 10279 240
+3 24102 764
+4 12383 4173
+5 13861 15918
+6 21327 1046
+7 5288 14579
+8 28158 8069
+9 16583 11098
+10 16681 28363
+11 13980 24725
+12 32169 17989
+13 10907 2767
+14 21557 3818
+15 26676 12422
+16 7676 8754
+17 14905 20232
+18 15719 24646
+19 31942 8589
+20 19978 27197
+21 27060 15071
+22 6071 26649
+23 10393 11176
+24 9597 13370
+25 7081 17677
+26 1433 19513
+27 26925 9014
+28 19202 8900
+29 18152 30647
+30 20803 1737
+31 11804 25221
+32 31683 17783
+33 29694 9345
+34 12280 26611
+35 6526 26122
+36 26165 11241
+37 7666 26962
+38 16290 8480
+39 11774 10120
+40 30051 30426
+41 1335 15424
+42 6865 17742
+43 31779 12489
+44 32120 21001
+45 14508 6996
+46 979 25024
+47 4554 21896
+48 7989 21777
+49 4972 20661
+50 6612 2730
+51 12742 4418
+52 29194 595
+53 19267 20113"""
+
+
+@lru_cache(maxsize=1)
+def dvbs2_12() -> SparseCode:
+    """DVB-S2 normal-frame rate-1/2 LDPC code (n = 64800, k = 32400, E = 226,799): BASELINE config [4]."""
+    groups = [np.array(list(map(int, line.split())), np.int64) for line in _DVBS2_N_12.splitlines()]
+    return _ira_code(groups, "dvbs2_12")
+
+
+def dvbs2_shaped(seed: int = 2019) -> SparseCode:
+    """A DVB-S2-SHAPED normal-frame rate-1/2 IRA code: the structure, degree profile and edge count
+    (E = 226,799) of :func:`dvbs2_12` (n = 64800, k = 32400, q = 90, 36 rows of degree 8, 54 of degree 3)
+    with seeded pseudo-random addresses.  Kept as a second large test code (no 802.11n-like regularity).
+
+    Each residue class mod q receives exactly 5 addresses, distinct inside a row, as in the standard."""
+    q, Z = 90, 360
     rng = np.random.default_rng(seed)
     degs = [8] * 36 + [3] * 54
-    # residues: each class 0..q-1 used exactly 5 times, distinct inside a row
     while True:
         pool = np.repeat(np.arange(q), 5)
         rng.shuffle(pool)
@@ -406,25 +535,7 @@ def dvbs2_shaped(seed: int = 2019) -> SparseCode:
         if ok:
             break
     groups = [r + q * rng.integers(0, Z, size=len(r)) for r in rows]
-    cols, chks = [], []
-    i = np.arange(Z)
-    for g, xs in enumerate(groups):
-        for x in xs:
-            chks.append((x + i * q) % m)
-            cols.append(g * Z + i)
-    # parity: check c touches parity bits c-1 (if c > 0) and c
-    c = np.arange(m)
-    chks += [c, c[1:]]
-    cols += [k + c, k + c[1:] - 1]
-    chks = np.concatenate(chks)
-    cols = np.concatenate(cols)
-    order = np.lexsort((cols, chks))
-    chks, cols = chks[order], cols[order]
-    row_ptr = np.zeros(m + 1, np.int64)
-    np.add.at(row_ptr, chks + 1, 1)
-    row_ptr = np.cumsum(row_ptr).astype(np.int32)
-    return SparseCode(m, n, row_ptr, cols.astype(np.int32), name="dvbs2s_12",
-                      info_groups=np.array([np.pad(g, (0, 8 - len(g)), constant_values=-1) for g in groups]))
+    return _ira_code(groups, "dvbs2s_12")
 
 
 class IRAEncoder:

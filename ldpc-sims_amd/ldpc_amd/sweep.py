@@ -132,6 +132,26 @@ PKL_KEYS = ("snrdb", "uncoded_ber", "coded_ber", "coded_bler",
             "wmse_nn", "wmse_quantized")
 
 
+def ebn0_at(snr_db, curve, level):
+    """Eb/N0 (dB) where a monotone error-rate curve crosses ``level``: linear interpolation of log10(rate)
+    between the two grid points that bracket it (points with rate 0 are dropped).  None if not bracketed."""
+    x = np.asarray(snr_db, np.float64)
+    y = np.asarray(curve, np.float64)
+    keep = y > 0
+    x, ly, t = x[keep], np.log10(y[keep]), np.log10(level)
+    for i in range(len(x) - 1):
+        if ly[i] >= t >= ly[i + 1] and ly[i] != ly[i + 1]:
+            return float(x[i] + (ly[i] - t) * (x[i + 1] - x[i]) / (ly[i] - ly[i + 1]))
+    return None
+
+
+def ebn0_offset_db(snr_db, curve, ref_curve, level):
+    """Horizontal distance (dB) of ``curve`` from ``ref_curve`` at error rate ``level``: positive = curve
+    needs more Eb/N0 than the reference for the same rate.  The quantity north_star bounds by +-0.05 dB."""
+    a, b = ebn0_at(snr_db, curve, level), ebn0_at(snr_db, ref_curve, level)
+    return None if a is None or b is None else a - b
+
+
 def save(result: dict, path: str):
     """``.pkl``: the reference's schema — all 12 keys of ``evaluate_quantized.py:155-172`` as float64
     numpy arrays of one entry per SNR point, so ``plots.py`` reads the file unchanged.  The ``*_nn`` keys
@@ -177,9 +197,17 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LDPC_BENCH_SHARE_GPU / LDPC_BENCH_BACKEND (as in bench.py) only rehearse N>1 ranks on a 1-GPU box
+    # (ranks share cuda:0, counters over gloo); real multi-GPU runs use one GPU per rank and RCCL.
+    if os.environ.get("LDPC_BENCH_SHARE_GPU"):
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("LDPC_BENCH_BACKEND", "nccl")  # nccl == RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     r = run(a.code, a.algo, a.iters, a.clamp, a.alpha, a.beta, _parse_points(a.snr), a.n, a.batch, a.seed,
             rank, world, local, a.early_stop, mod=a.mod, adc_bits=a.adc_bits, clip_ratio=a.clip_ratio)
     if rank == 0:

@@ -21,10 +21,11 @@ What it records (all .npz, numeric arrays only — loadable with allow_pickle=Fa
                            pins the reference's LLR formula/sign convention for the channel front end.
   * adc_quantizer.npz      ``quantizer`` (``:37-51``) at fixed clips (incl. the lo > hi corner) and
                            ``gen_qdata`` (``:118-128``, AGC clip = std * ratio) on a complex64-valued stream.
+  * bp_x0.npz              the forward with non-zero initial messages x (bp/bp.py:43-47).
   * bp_weighted_peg64.npz  weighted BP: the reference module with random per-layer ``input_weight`` /
                            ``llr_weight`` set in memory (``bp_vc.py:19,24``), 5 iterations, fp32 and fp64.
 
-    python tests/golden/make_golden.py [bp] [adc] [weighted]     (no argument: all)
+    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0]     (no argument: all)
 """
 import os
 import sys
@@ -262,8 +263,37 @@ def gen_wifi_sp():
                             snrs=np.array(snrs), **rec)
 
 
+def gen_x0():
+    """bp_x0.npz: the reference forward with NON-ZERO initial messages x (bp/bp.py:43-47), which the first
+    layer consumes like any later one: (64,32) at iterations 0 / 1 / 5 and (648,1/2) at 3, clamp 10, x drawn
+    N(0, 2^2) per edge (check-order, masking.py:84-88), fp32 module and .double()."""
+    from ldpc_amd.codes import get_code
+    rec = {}
+    for name, iters_list, B in (("peg64_32", (0, 1, 5), 64), ("wifi648_12", (3,), 16)):
+        H = parity.H.astype(np.int64) if name == "peg64_32" else np.asarray(get_code(name)[0], np.int64)
+        enc = Encoder(H)
+        rng = np.random.default_rng(4040 + H.shape[1])
+        cw = enc.encode(rng.integers(0, 2, size=(B, enc.k)))
+        llr = bpsk_awgn_llr(cw.astype(np.float64), 2.0, enc.k / H.shape[1], rng)
+        E = int(H.sum())
+        x = (2.0 * rng.standard_normal((B, E))).astype(np.float32)
+        rec[f"{name}_llr"] = llr
+        rec[f"{name}_x"] = x
+        for iters in iters_list:
+            model = BeliefPropagation(H, iters)
+            model.eval()
+            with torch.no_grad():
+                p32 = model(torch.tensor(x), torch.tensor(llr), 10.0).numpy()
+                m64 = model.double()
+                p64 = m64(torch.tensor(x, dtype=torch.float64), torch.tensor(llr, dtype=torch.float64), 10.0).numpy()
+            rec[f"{name}_it{iters}_p1_f32"] = p32.astype(np.float32)
+            rec[f"{name}_it{iters}_p1_f64"] = p64
+            print("x0", name, iters, "ref f32 vs f64 |dp1| max", float(np.abs(p32 - p64).max()), flush=True)
+    np.savez_compressed(os.path.join(HERE, "bp_x0.npz"), clamp=10.0, **rec)
+
+
 if __name__ == "__main__":
-    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi"]
+    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0"]
     for part in parts:
-        {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp}[part]()
+        {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp, "x0": gen_x0}[part]()
     print("done")

@@ -72,3 +72,37 @@ def test_dvbs2_shaped_structure_and_encoder():
     cw = IRAEncoder(c).encode(np.random.default_rng(0).integers(0, 2, size=(2, c.k)))
     for row in cw:
         assert not (np.add.reduceat(row[c.col_idx].astype(np.int64), c.row_ptr[:-1]) % 2).any()
+
+
+def test_dvbs2_table_structure():
+    """EN 302 307 rate-1/2 table (codes._DVBS2_N_12): structural checks that catch a mistyped address.
+    The reference cannot build a code this size (masking.py:36-38), so its contents are unpinned."""
+    from collections import Counter
+    from ldpc_amd.codes import IRAEncoder, _DVBS2_N_12, dvbs2_12
+    rows = [list(map(int, ln.split())) for ln in _DVBS2_N_12.splitlines()]
+    assert [len(r) for r in rows] == [8] * 36 + [3] * 54
+    assert all(0 <= x < 32400 for r in rows for x in r)
+    # the first address of each row is its own residue class (54..89, then 0..53)
+    assert [r[0] for r in rows] == list(range(54, 90)) + list(range(54))
+    # every residue class mod q = 90 receives exactly 5 addresses -> every check has 5 info edges
+    assert set(Counter(x % 90 for r in rows for x in r).values()) == {5}
+    c = dvbs2_12()
+    g = Graph.from_H(c)
+    assert (c.m, c.n, g.E) == (32400, 64800, 226799)
+    dc = np.bincount(g.check_degrees())
+    assert dc[7] == 32399 and dc[6] == 1
+    dv = np.bincount(g.var_degrees())
+    assert dv[8] == 12960 and dv[3] == 19440 and dv[2] == 32399 and dv[1] == 1
+    # no repeated edge, no 4-cycle (two columns sharing two checks): girth >= 6
+    key = g.edge_check.astype(np.int64) * c.n + g.col_idx
+    assert len(np.unique(key)) == g.E
+    pairs = []
+    for cc in range(c.m):
+        v = g.col_idx[g.row_ptr[cc]:g.row_ptr[cc + 1]].astype(np.int64)
+        a, b = np.triu_indices(len(v), 1)
+        pairs.append(v[a] * c.n + v[b])
+    p = np.concatenate(pairs)
+    assert len(np.unique(p)) == len(p)
+    cw = IRAEncoder(c).encode(np.random.default_rng(1).integers(0, 2, size=(2, c.k)))
+    for row in cw:
+        assert not (np.add.reduceat(row[c.col_idx].astype(np.int64), c.row_ptr[:-1]) % 2).any()

@@ -1,0 +1,80 @@
+"""The product path multi-rank: bench.py and ``python -m ldpc_amd.sweep`` as 2 ranks with the HIP decoder
+in the loop.  Each rank is a FRESH child process (subprocess; the test process never execs); both share
+cuda:0 (LDPC_BENCH_SHARE_GPU) and reduce their counters over gloo (LDPC_BENCH_BACKEND) — on the driver's
+8-GPU node the same code runs one GPU per rank over RCCL.  This covers what the oracle-decoded gloo test
+(test_dist.py) cannot: the rank-offset LLR generation (``rank * B`` into ldpc_random_bits /
+ldpc_awgn_llr), ``max_over_ranks`` and the counter all-reduce of device tensors.  The union of the two
+shards is the same data as one process decoding both, so the summed counts must be EQUAL.
+Reference multi-GPU mode: nn.DataParallel, pytorch/ofdm/ofdm_functions.py:141-145."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch(args, world, timeout=240):
+    """Start ``world`` ranks of ``python <args>`` as child processes; return rank 0's stdout."""
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LDPC_BENCH_SHARE_GPU="1",
+                   LDPC_BENCH_BACKEND="gloo", PYTHONPATH=os.path.join(ROOT, "ldpc-sims_amd"))
+        if world == 1:
+            for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+                env.pop(k)
+        procs.append(subprocess.Popen([sys.executable, *args], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=timeout)
+            assert p.returncode == 0, e[-3000:]
+            outs.append(o)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return outs[0]
+
+
+def _bench_line(out):
+    return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+
+
+def test_bench_two_ranks_equal_one_process_over_both_shards():
+    common = ["bench.py", "--steps", "2", "--warmup", "1", "--iters", "10", "--ebn0", "1:1:3",
+              "--no-cpu-baseline"]
+    two = _bench_line(_launch([*common, "--gpus", "2", "--batch", "4096"], 2))
+    one = _bench_line(_launch([*common, "--gpus", "1", "--batch", "8192"], 1))
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 8192 and two["value"] > 0
+    assert two["ber"]["codewords_per_point"] == one["ber"]["codewords_per_point"] == 8192
+    assert two["ber"]["coded_ber_info"] == one["ber"]["coded_ber_info"]
+    assert two["ber"]["coded_bler"] == one["ber"]["coded_bler"]
+    assert 0 < one["ber"]["coded_bler"][0] < 1   # a point with errors, so equal counts mean something
+
+
+def test_sweep_two_ranks_equal_one_process(tmp_path):
+    common = ["-m", "ldpc_amd.sweep", "--code", "wifi648_12", "--algo", "minsum", "--iters", "10",
+              "--snr", "1:1:3", "--n", "10000", "--batch", "3000", "--seed", "4"]
+    _launch([*common, "--out", str(tmp_path / "two.json")], 2)
+    _launch([*common, "--out", str(tmp_path / "one.json")], 1)
+    two = json.load(open(tmp_path / "two.json"))
+    one = json.load(open(tmp_path / "one.json"))
+    assert two["codewords"] == one["codewords"] == [10000] * 3
+    for key in ("uncoded_ber", "coded_ber", "coded_bler"):
+        assert two[key] == one[key], key

@@ -9,6 +9,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 from ldpc_amd.sweep import run  # noqa: E402
+from softparity import _log  # noqa: E402
 
 SNR = list(range(11))
 PUB_UNCODED = [0.15891, 0.13101, 0.10402, 0.07875, 0.05647, 0.03750, 0.02295, 0.01258, 0.00595, 0.00240, 0.00077]
@@ -118,5 +119,7 @@ def test_ber_overlay_in_db():
             tol = max(0.05, 3 * sig)
             rows.append((kind, lv, off, sig, tol))
             print(f"overlay {kind}@{lv:g}: offset {off:+.4f} dB (1-sigma {sig:.4f} dB, bound {tol:.3f} dB)")
+            _log({"label": "ber_overlay_db", "kind": kind, "level": lv, "offset_db": off, "sigma_db": sig,
+                  "bound_db": tol, "codewords_gpu": n, "codewords_published": N})
     for kind, lv, off, sig, tol in rows:
         assert off is not None and abs(off) <= tol, (kind, lv, off, tol)

@@ -15,7 +15,8 @@ _RUNS = [("sp32", "float", 0, 0), ("sp32_es", "float", 0, 1), ("sp64", "double",
          ("ms32", "float", 1, 0), ("ms32_es", "float", 1, 1)]
 SRCS = [("abi.hip", "abi.hip.o", []), ("generic.hip", "generic.hip.o", [])] + [
     ("generic_run.hip", f"generic_run_{n}.o", [f"-DRUN_T={t}", f"-DRUN_MS={ms}", f"-DRUN_ES={es}", f"-DRUN_NAME=generic_run_{n}"])
-    for (n, t, ms, es) in _RUNS] + [("qc.hip", "qc.hip.o", []), ("qc_sl.hip", "qc_sl.hip.o", []), ("channel.hip", "channel.hip.o", [])]
+    for (n, t, ms, es) in _RUNS] + [("qc.hip", "qc.hip.o", []), ("qc_sl.hip", "qc_sl.hip.o", []), ("qc_pk.hip", "qc_pk.hip.o", []),
+           ("channel.hip", "channel.hip.o", [])]
 OUT = os.path.join(HERE, "ldpc_amd", "libldpc_hip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off",  # min-sum must round exactly like oracle/ldpc_oracle.c (no FMA contraction)
@@ -29,7 +30,8 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
 # iterative-ilp scheduling: +2 % on the (648,1/2) stored min-sum loop (A/B, 34.4 -> 35.1 M cw/s), same code
 # otherwise (the loop is latency- and issue-limited at the 128-VGPR / 4-waves budget).
 SCHED = ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"]
-PER_FILE = {"qc.hip": ["-fno-honor-nans", *SCHED], "qc_sl.hip": ["-fno-honor-nans", *SCHED]}
+PER_FILE = {"qc.hip": ["-fno-honor-nans", *SCHED], "qc_sl.hip": ["-fno-honor-nans", *SCHED],
+            "qc_pk.hip": ["-fno-honor-nans"]}  # iterative-ilp crashes the register allocator on qc_pk (ROCm 7.2)
 
 
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), per_file=True, qc_flags=None) -> str:

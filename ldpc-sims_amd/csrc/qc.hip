@@ -21,14 +21,8 @@
 
 namespace ldpc {
 
-#ifndef QC_DIAG_DPP
-#define QC_DIAG_DPP 0
-#endif
 #ifndef QC_DIAG_NO_L
 #define QC_DIAG_NO_L 0
-#endif
-#ifndef QC_DIAG_NOSEL
-#define QC_DIAG_NOSEL 0
 #endif
 #ifndef QC_DIAG_NOCMP
 #define QC_DIAG_NOCMP 0
@@ -56,42 +50,6 @@ struct QCSpec {
     int (*launch_ms)(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
                      hipStream_t st);
 };
-
-// lanes whose lifting index z lies in [lo, hi), in each codeword's lane group
-template <int Z, int CPW>
-constexpr uint64_t lane_range_mask(int lo, int hi) {
-    uint64_t m = 0;
-    for (int z = lo; z < hi; ++z) {
-        m |= 1ull << z;
-        if (CPW == 2) m |= 1ull << (32 + z);
-    }
-    return m;
-}
-
-// lane in MASK ? b : a.  The mask is a compile-time SGPR-pair constant, so the select is one VALU op
-// with no v_cmp (and no VCC hazard).  Volatile: never CSE'd across rows or hoisted out of the loop.
-template <uint64_t MASK>
-__device__ __forceinline__ int sel_lanes(int a, int b) {
-#if QC_DIAG_NOSEL
-    (void)b;  // DIAGNOSTIC BUILD ONLY (wrong results): no wrap select, to price the address selects
-    return a;
-#else
-    int r;
-    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(MASK));
-    return r;
-#endif
-}
-
-__device__ __forceinline__ float bperm(int addr, float v) {
-#if QC_DIAG_DPP
-    // DIAGNOSTIC BUILD ONLY (wrong results): a VALU DPP move instead of the LDS-pipe permute, to price
-    // the ds_bpermute traffic.  The address stays live so its computation is still timed.
-    asm volatile("" ::"v"(addr));
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, false));
-#else
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
-#endif
-}
 
 // QUANT = false: float min-sum.  QUANT = true: integer offset min-sum carried in float registers (all
 // values are small integers, so every add/sub is exact and equals the oracle's int arithmetic).
@@ -312,24 +270,12 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
 #ifndef QC_ST_WAVES_PER_SIMD
 #define QC_ST_WAVES_PER_SIMD 4  // 128 VGPRs; measured 30.6M cw/s vs 26.2M at 3 waves (648, 50 it)
 #endif
-
-// Lane-mask rotation for the early-stop syndrome: bit i of the result = bit (i + S) mod Z of x, in each
-// codeword's lane group (CPW == 2: two 27-bit groups at bits 0 and 32).  Wave-uniform: scalar ALU.
-// Bits outside the groups are garbage; the caller masks once per row.
-template <int Z, int CPW, int S>
-__device__ __forceinline__ uint64_t rot_lanes(uint64_t x) {
-    if constexpr (S == 0) {
-        return x;
-    } else if constexpr (CPW == 1) {
-        return (x >> S) ^ (x << (Z - S));
-    } else {
-        const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-        return ((uint64_t)((hi >> S) ^ (hi << (Z - S))) << 32) | (uint32_t)((lo >> S) ^ (lo << (Z - S)));
-    }
-}
+#ifndef QC_ST_WAVES_PER_SIMD_EARLY
+#define QC_ST_WAVES_PER_SIMD_EARLY 4  // early stop keeps APP_it and the syndrome ballots live
+#endif
 
 template <class C, bool QUANT, bool EARLY, int NORM>
-__global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const float* __restrict__ llr, int64_t B, int iters,
+__global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const float* __restrict__ llr, int64_t B, int iters,
                                                                        float clamp, float alpha, float beta, float qmax,
                                                                        float app_max, float qinv, int flags,
                                                                        uint8_t* __restrict__ bits, float* __restrict__ soft,
@@ -481,6 +427,9 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
             // sign of the product folded into the two magnitudes once per row
             const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);
             const float M2 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn2, alpha, beta, clamp)) ^ tot);
+            // NORM_PLAIN: compare-free select as in k_qc_ms_ph (med3 of the unsigned magnitudes, XOR)
+            const float A1 = mag_of<NORM>(mn1, alpha, beta, clamp), A2 = mag_of<NORM>(mn2, alpha, beta, clamp);
+            const uint32_t X = __float_as_uint(M1) ^ __float_as_uint(A2);
 #if !QC_L128
             int lr = lrow;
             asm volatile("" : "+v"(lr));
@@ -491,10 +440,17 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
                 // |v| == min1 picks the min slot; ties imply min2 == min1 (bit-exact, see k_qc_ms)
 #if QC_DIAG_NOCMP
                 const float mg = M1;  // DIAGNOSTIC BUILD ONLY (wrong results): prices the argmin select
-#else
-                const float mg = (fabsf(v[t]) == mn1) ? M2 : M1;
-#endif
                 const float c = __uint_as_float(__float_as_uint(mg) ^ (__float_as_uint(v[t]) & 0x80000000u));
+#else
+                float c;
+                if constexpr (NORM == NORM_PLAIN) {
+                    const uint32_t m = __float_as_uint(__builtin_amdgcn_fmed3f(fabsf(v[t]), A1, A2));
+                    c = __uint_as_float((X ^ m) ^ (__float_as_uint(v[t]) & 0x80000000u));
+                } else {
+                    const float mg = (fabsf(v[t]) == mn1) ? M2 : M1;
+                    c = __uint_as_float(__float_as_uint(mg) ^ (__float_as_uint(v[t]) & 0x80000000u));
+                }
+#endif
                 float cr;
                 if constexpr (s == 0) {
                     cr = c;
@@ -564,20 +520,18 @@ __global__ __launch_bounds__(256, QC_ST_WAVES_PER_SIMD) void k_qc_ms_st(const fl
 #ifndef QC_PH_WAVES_PER_SIMD
 #define QC_PH_WAVES_PER_SIMD 4
 #endif
-
-template <class C>
-constexpr int rot_uses(int rho) {  // ds_bpermutes per iteration that read lane (z + rho) mod Z
-    int n = 0;
-    for (int r = 0; r < C::MB; ++r)
-        for (int t = 0; t < C::DEG[r]; ++t) {
-            const int s = C::SHR[r][t];
-            n += (s != 0 && (s == rho || C::Z - s == rho));
-        }
-    return n;
-}
+#ifndef QC_PH_SKEW
+#define QC_PH_SKEW 0
+#endif
+#ifndef QC_PH_SCHED
+#define QC_PH_SCHED 0  // > 0: interleave one LDS op per QC_PH_SCHED VALU in the loop (sched_group_barrier)
+#endif
+#ifndef QC_PH_WAVES_PER_SIMD_EARLY
+#define QC_PH_WAVES_PER_SIMD_EARLY 3  // spill-free (145 VGPRs): 648 min-sum early stop 24.6 -> 57.9 M cw/s (A/B)
+#endif
 
 template <class C, bool QUANT, bool EARLY, int NORM>
-__global__ __launch_bounds__(256, QC_PH_WAVES_PER_SIMD) void k_qc_ms_ph(const float* __restrict__ llr, int64_t B, int iters,
+__global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAVES_PER_SIMD) void k_qc_ms_ph(const float* __restrict__ llr, int64_t B, int iters,
                                                                        float clamp, float alpha, float beta, float qmax,
                                                                        float app_max, float qinv, int flags,
                                                                        uint8_t* __restrict__ bits, float* __restrict__ soft,
@@ -707,6 +661,10 @@ __global__ __launch_bounds__(256, QC_PH_WAVES_PER_SIMD) void k_qc_ms_ph(const fl
         });
     };
 
+#if QC_PH_SKEW
+    // A/B: desynchronise the waves sharing a CU's LDS pipe (odd waves start about half an iteration late)
+    if ((threadIdx.x >> 6) & 1) __builtin_amdgcn_s_sleep(QC_PH_SKEW);
+#endif
     int it = 0;
     for (; it + 1 < iters; ++it) {
         cn_phase();
@@ -752,6 +710,14 @@ __global__ __launch_bounds__(256, QC_PH_WAVES_PER_SIMD) void k_qc_ms_ph(const fl
                 constexpr int p = decltype(pp)::value;
                 v2c_col(std::integral_constant<int, lcol<C>(p)>{}, vn_col(pp));
             });
+#if QC_PH_SCHED
+            // scheduling hint (A/B): spread the LDS rotations evenly through the VALU stream instead of
+            // bursts of one row's gathers, so a wave rarely stalls on a full LDS queue
+            static_for<0, 100>([&](auto) __attribute__((always_inline)) {
+                __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);           // one DS instruction
+                __builtin_amdgcn_sched_group_barrier(0x002, QC_PH_SCHED, 0); // then N VALU
+            });
+#endif
         }
     }
     // last iteration (or early exit): outputs straight from the VN phase, column by column
@@ -793,6 +759,9 @@ __global__ __launch_bounds__(256, QC_PH_WAVES_PER_SIMD) void k_qc_ms_ph(const fl
 #ifndef QC_SP_WAVES_PER_SIMD
 #define QC_SP_WAVES_PER_SIMD 4
 #endif
+#ifndef QC_SP_WAVES_PER_SIMD_EARLY
+#define QC_SP_WAVES_PER_SIMD_EARLY 2  // 648 tanh-SP early stop 10.2 -> 12.1 M cw/s (A/B; 3 waves: 11.1)
+#endif
 
 // Early stop (EARLY): before iteration it >= 1, the hard decisions of z_it = 0.5 * (L + ascending sum of
 // c2v) — the generic VN kernel's hb, same operations — are balloted per block column and rotated into
@@ -800,7 +769,7 @@ __global__ __launch_bounds__(256, QC_PH_WAVES_PER_SIMD) void k_qc_ms_ph(const fl
 // iters_used = it and its z_it is parked in its own L region of LDS (its lanes keep computing for the
 // wave's other codeword, discarded).  Bitwise equal to the generic path's early stop.
 template <class C, bool EARLY>
-__global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const float* __restrict__ llr, int64_t B, int iters,
+__global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const float* __restrict__ llr, int64_t B, int iters,
                                                                        float clamp, int flags, uint8_t* __restrict__ bits,
                                                                        float* __restrict__ soft, int32_t* __restrict__ iters_used) {
     constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
@@ -966,6 +935,15 @@ __global__ __launch_bounds__(256, QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const fl
     }
 }
 
+// packed quantized kernels (qc_pk.hip)
+int qc_launch_qms_pk_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                                int32_t* used, hipStream_t st);
+int qc_launch_qms_pk_wifi1296_23(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                                 int32_t* used, hipStream_t st);
+#ifndef QC_PACKED
+#define QC_PACKED 1  // quantized min-sum for Z <= 64 runs the packed fp16 kernel (0: float-register kernels, A/B)
+#endif
+
 // sliced kernels for Z > 64 (qc_sl.hip)
 int qc_launch_sl_wifi1944_56(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
                               int32_t* used, hipStream_t st);
@@ -990,7 +968,13 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     if (p.algo == LDPC_ALGO_TANH_SP) {
         if (es) k_qc_sp_st<C, true><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
         else k_qc_sp_st<C, false><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+    } else if (p.algo == LDPC_ALGO_QMIN_SUM && QC_PACKED != 0) {
+        // two codewords per lane in packed fp16 (qc_pk.hip)
+        if constexpr (std::is_same_v<C, Wifi648_12>) return qc_launch_qms_pk_wifi648_12(llr, B, p, bits, soft, used, st);
+        else if constexpr (std::is_same_v<C, Wifi1296_23>) return qc_launch_qms_pk_wifi1296_23(llr, B, p, bits, soft, used, st);
+        else return set_error(LDPC_EUNSUPPORTED, "no packed quantized kernel for %s", C::NAME);
     } else if (p.algo == LDPC_ALGO_QMIN_SUM) {
+#if !QC_PACKED  // the float-register quantized kernels (A/B builds only)
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
 #define QL(E, N)                                                                                                  \
     do {                                                                                                          \
@@ -1004,6 +988,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         if (b != 0.0f) { if (es) QL(true, NORM_BETA); else QL(false, NORM_BETA); }
         else           { if (es) QL(true, NORM_PLAIN); else QL(false, NORM_PLAIN); }
 #undef QL
+#endif
     } else {
         const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
 #define FL(E, N)                                                                                                  \

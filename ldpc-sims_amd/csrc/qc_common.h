@@ -162,4 +162,74 @@ constexpr int col_edge(int j, int k) {  // k-th edge of block column j in ascend
     return -1;
 }
 
+// ---- lane rotations (ds_bpermute) shared by the register kernels ----------------------------------
+#ifndef QC_DIAG_DPP
+#define QC_DIAG_DPP 0
+#endif
+#ifndef QC_DIAG_NOSEL
+#define QC_DIAG_NOSEL 0
+#endif
+
+// lanes whose lifting index z lies in [lo, hi), in each codeword's lane group
+template <int Z, int CPW>
+constexpr uint64_t lane_range_mask(int lo, int hi) {
+    uint64_t m = 0;
+    for (int z = lo; z < hi; ++z) {
+        m |= 1ull << z;
+        if (CPW == 2) m |= 1ull << (32 + z);
+    }
+    return m;
+}
+
+// lane in MASK ? b : a.  The mask is a compile-time SGPR-pair constant, so the select is one VALU op
+// with no v_cmp (and no VCC hazard).  Volatile: never CSE'd across rows or hoisted out of the loop.
+template <uint64_t MASK>
+__device__ __forceinline__ int sel_lanes(int a, int b) {
+#if QC_DIAG_NOSEL
+    (void)b;  // DIAGNOSTIC BUILD ONLY (wrong results): no wrap select, to price the address selects
+    return a;
+#else
+    int r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(MASK));
+    return r;
+#endif
+}
+
+__device__ __forceinline__ float bperm(int addr, float v) {
+#if QC_DIAG_DPP
+    // DIAGNOSTIC BUILD ONLY (wrong results): a VALU DPP move instead of the LDS-pipe permute, to price
+    // the ds_bpermute traffic.  The address stays live so its computation is still timed.
+    asm volatile("" ::"v"(addr));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, false));
+#else
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+#endif
+}
+
+// Lane-mask rotation for the early-stop syndrome: bit i of the result = bit (i + S) mod Z of x, in each
+// codeword's lane group (CPW == 2: two 27-bit groups at bits 0 and 32).  Wave-uniform: scalar ALU.
+// Bits outside the groups are garbage; the caller masks once per row.
+template <int Z, int CPW, int S>
+__device__ __forceinline__ uint64_t rot_lanes(uint64_t x) {
+    if constexpr (S == 0) {
+        return x;
+    } else if constexpr (CPW == 1) {
+        return (x >> S) ^ (x << (Z - S));
+    } else {
+        const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+        return ((uint64_t)((hi >> S) ^ (hi << (Z - S))) << 32) | (uint32_t)((lo >> S) ^ (lo << (Z - S)));
+    }
+}
+
+template <class C>
+constexpr int rot_uses(int rho) {  // ds_bpermutes per iteration that read lane (z + rho) mod Z
+    int n = 0;
+    for (int r = 0; r < C::MB; ++r)
+        for (int t = 0; t < C::DEG[r]; ++t) {
+            const int s = C::SHR[r][t];
+            n += (s != 0 && (s == rho || C::Z - s == rho));
+        }
+    return n;
+}
+
 }  // namespace ldpc

@@ -1,0 +1,354 @@
+// qc_pk.hip — quantized (integer offset) min-sum for the 802.11n QC codes with Z <= 64: TWO codewords per
+// lane, packed as an fp16 pair in every register.
+//
+// The quantized decoder's values are small integers: LLRs and messages in [-qmax, qmax] (qmax <= 127),
+// posteriors L + sum c2v in [-(1 + d_v) qmax, (1 + d_v) qmax] before the app_max clamp — at most 1651 for the
+// 802.11n column degrees (<= 12), inside fp16's exact-integer range (2048).  So fp16 arithmetic on them is
+// exact and equals the oracle's int arithmetic (oracle/ldpc_oracle.c qms_one) operation for operation, and
+// one v_pk_* instruction advances two codewords.  The lane rotations (ds_bpermute, the LDS pipe that bounds
+// the float kernels) move 32 bits per lane, i.e. both codewords at once: half the LDS traffic per codeword.
+//
+// Structure: k_qc_ms_ph's phased flooding iteration (qc.hip) —
+//   CN phase, row by row: v2c (variable frame) gathered into the check frame in place; |v| by masking the
+//     two sign bits; the two smallest magnitudes; the sign product; c2v in the check frame.
+//   VN phase, column by column: c2v rotated back; APP_j = sat(L_j + sum c2v, app_max); v2c = sat(APP_j - c2v,
+//     qmax) for the next iteration.
+// Check-node output without a compare (every |v| >= mn1, magnitudes are non-negative and +0 only):
+//   min(|v|, mn2) is mn1 for the argmin slot and mn2 for every other slot (ties: mn1 == mn2), so XOR-ing it
+//   with mn1 ^ mn2 yields the OTHER minimum bit for bit; offset beta is applied to |v| first,
+//   max(|v| - beta, 0), which is monotone, so the order statistics of the offset magnitudes are the offset
+//   order statistics (oracle: mag = max(min - beta, 0)).  A -0 v2c (the sign of a zero) changes only the sign
+//   of zero-magnitude outputs, so every value equals the oracle's.
+// Lane layout: lane (half, z) of wave w holds lifting index z of codewords 2(w*CPW + half) (low fp16) and
+// 2(w*CPW + half) + 1 (high), CPW = 2 for Z <= 32 (lane halves), else 1.  The lane frames (PHI) and the
+// rotation tables are qc_tables.h's, as in the float kernels.
+#include "qc_common.h"
+
+namespace ldpc {
+
+#ifndef QC_PK_WAVES_PER_SIMD
+#define QC_PK_WAVES_PER_SIMD 4
+#endif
+#ifndef QC_PK_WAVES_PER_SIMD_EARLY
+#define QC_PK_WAVES_PER_SIMD_EARLY 3
+#endif
+#ifndef QC_PK_ADDR_MIN_USES
+#define QC_PK_ADDR_MIN_USES 3  // Z <= 32: rotations used this often per iteration keep their address in a register
+#endif
+#ifndef QC_PK_ADDR_MIN_USES_Z64
+#define QC_PK_ADDR_MIN_USES_Z64 4  // Z > 32 (one lane group): 6 address registers at 4 uses (18 at 3)
+#endif
+#define QC_PK_TPB 256
+
+using h2 = _Float16 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2 as_h2(uint32_t x) { return __builtin_bit_cast(h2, x); }
+__device__ __forceinline__ uint32_t as_u(h2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t pmin(uint32_t a, uint32_t b) { return as_u(__builtin_elementwise_min(as_h2(a), as_h2(b))); }
+__device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b) { return as_u(__builtin_elementwise_max(as_h2(a), as_h2(b))); }
+__device__ __forceinline__ uint32_t padd(uint32_t a, uint32_t b) { return as_u(as_h2(a) + as_h2(b)); }
+__device__ __forceinline__ uint32_t psub(uint32_t a, uint32_t b) { return as_u(as_h2(a) - as_h2(b)); }
+__device__ __forceinline__ uint32_t pbperm(int addr, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v); }
+__device__ __forceinline__ uint32_t pk2(float lo, float hi) { return as_u(h2{(_Float16)lo, (_Float16)hi}); }
+constexpr uint32_t kSign2 = 0x80008000u, kMag2 = 0x7fff7fffu;
+
+template <class C>
+constexpr int max_col_deg() {
+    int m = 0;
+    for (int j = 0; j < C::NB; ++j) m = col_deg<C>(j) > m ? col_deg<C>(j) : m;
+    return m;
+}
+template <class C>
+constexpr int min_row_deg() {
+    int m = 1 << 30;
+    for (int r = 0; r < C::MB; ++r) m = C::DEG[r] < m ? C::DEG[r] : m;
+    return m;
+}
+
+// the two smallest of D packed non-negative magnitudes (each result is one of the inputs, bit for bit)
+template <int D>
+__device__ __forceinline__ void two_min_pk(const uint32_t (&a)[D], uint32_t& mn1, uint32_t& mn2) {
+    static_assert(D >= 2, "packed min-sum: check degree >= 2");
+    mn1 = pmin(a[0], a[1]);
+    mn2 = pmax(a[0], a[1]);
+    static_for<2, D>([&](auto tt) __attribute__((always_inline)) {
+        constexpr int t = decltype(tt)::value;
+        mn2 = pmin(mn2, pmax(mn1, a[t]));
+        mn1 = pmin(mn1, a[t]);
+    });
+}
+
+template <int D>
+__device__ __forceinline__ uint32_t xor_all_u(const uint32_t (&v)[D]) {
+    uint32_t t = v[0];
+    static_for<0, (D - 1) / 2>([&](auto pp) __attribute__((always_inline)) {
+        constexpr int k = 1 + 2 * decltype(pp)::value;
+        t = __builtin_amdgcn_bitop3_b32(t, v[k], v[k + 1], 0x96);
+    });
+    if constexpr ((D - 1) % 2) t ^= v[D - 1];
+    return t;
+}
+
+template <class C, bool EARLY, bool BETA>
+__global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_PK_WAVES_PER_SIMD) void k_qc_qms_pk(
+    const float* __restrict__ llr, int64_t B, int iters, float qmax, float app_max, float beta, float qinv, int flags,
+    uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
+    constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
+    constexpr int NE = edge_off<C>(MB);
+    static_assert(Z <= 64, "packed kernel: one lane group per codeword pair");
+    static_assert((1 + max_col_deg<C>()) * 127 < 2048, "fp16 must hold every posterior exactly");
+    static_assert(min_row_deg<C>() >= 2, "check degree >= 2");
+    constexpr int CPW = (Z <= 32) ? 2 : 1;
+    const int lane = threadIdx.x & 63;
+    const int half = (CPW == 2) ? (lane >> 5) : 0;
+    const int z = (CPW == 2) ? (lane & 31) : lane;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t cw0 = (wave * CPW + half) * 2;  // low fp16: cw0, high: cw0 + 1
+    const int zb = (z < Z) ? z : z - Z;
+    const int base4 = (half * 32 + zb) * 4;
+    const int base4m = base4 - 4 * Z;
+    using f4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int LSTR = lstr<C>();
+    __shared__ __attribute__((aligned(16))) uint32_t Ls[QC_PK_TPB * LSTR];  // lane-major packed L rows (lpos)
+    const int lrow = threadIdx.x * LSTR;
+
+    constexpr int MINU = (Z <= 32) ? QC_PK_ADDR_MIN_USES : QC_PK_ADDR_MIN_USES_Z64;
+    int ra[Z];
+    static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
+        constexpr int rho = decltype(rr)::value;
+        if constexpr (rot_uses<C>(rho) >= MINU)
+            ra[rho] = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(base4, base4m) + 4 * rho;
+    });
+    auto rot = [&](auto rr, uint32_t x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
+        constexpr int rho = decltype(rr)::value;
+        if constexpr (rho == 0) {
+            return x;
+        } else if constexpr (rot_uses<C>(rho) >= MINU) {
+            return pbperm(ra[rho], x);
+        } else {
+            return pbperm(sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(base4, base4m) + 4 * rho, x);
+        }
+    };
+    (void)ra;
+
+    // packed constants (SGPRs)
+    const uint32_t QM = pk2(qmax, qmax), NQM = pk2(-qmax, -qmax), AM = pk2(app_max, app_max), NAM = pk2(-app_max, -app_max);
+    const uint32_t BT = pk2(beta, beta);
+
+    // L = -sat(rint(llr / qstep), qmax) of both codewords (the float kernels' quantizer, in fp32), packed into
+    // this lane's LDS row; APP_0 = sat(L, app_max); v2c of iteration 0 = sat(APP_0 - 0, qmax)
+    uint32_t msg[NE];
+    {
+        const bool v0 = (z < Z) && (cw0 < B), v1 = (z < Z) && (cw0 + 1 < B);
+        uint32_t L[NB];
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            int t = z + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            const int64_t o = (int64_t)j * Z + t;
+            const float x0 = v0 ? llr[cw0 * N + o] : 0.0f;
+            const float x1 = v1 ? llr[(cw0 + 1) * N + o] : 0.0f;
+            const float q0 = fminf(fmaxf(rintf(x0 * qinv), -qmax), qmax);
+            const float q1 = fminf(fmaxf(rintf(x1 * qinv), -qmax), qmax);
+            L[j] = pk2(-q0, -q1);
+            Ls[lrow + lpos<C>(j)] = L[j];
+            L[j] = pmin(pmax(L[j], NAM), AM);
+        });
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                msg[edge_off<C>(r) + t] = pmin(pmax(L[C::COL[r][t]], NQM), QM);
+            });
+        });
+    }
+
+    // CN phase: v2c (variable frame) -> c2v (check frame), in place
+    auto cn_phase = [&]() __attribute__((always_inline)) {
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            constexpr int d = C::DEG[r];
+            constexpr int e0 = edge_off<C>(r);
+            uint32_t v[d], a[d];
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                v[t] = rot(std::integral_constant<int, C::SHR[r][t]>{}, msg[e0 + t]);
+                a[t] = v[t] & kMag2;
+                if constexpr (BETA) a[t] = pmax(psub(a[t], BT), 0u);  // max(|v| - beta, 0)
+            });
+            uint32_t mn1, mn2;
+            two_min_pk(a, mn1, mn2);
+            const uint32_t X = mn1 ^ mn2 ^ (xor_all_u(v) & kSign2);  // sign product folded in
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                const uint32_t other = X ^ pmin(a[t], mn2);
+                msg[e0 + t] = __builtin_amdgcn_bitop3_b32(other, v[t], kSign2, 0x78);  // other ^ (v & sign)
+            });
+        });
+    };
+    // VN phase, column j: c2v back to the variable frame, APP_j = sat(L_j + sum c2v, app_max)
+    f4 Lg;
+    auto vn_col = [&](auto pp) __attribute__((always_inline)) {
+        constexpr int p = decltype(pp)::value;
+        constexpr int j = lcol<C>(p);
+        constexpr int dj = col_deg<C>(j);
+        if constexpr (p % 4 == 0) {
+            int lr = lrow;
+            asm volatile("" : "+v"(lr));  // not hoisted out of the loop (register budget)
+            Lg = *static_cast<const f4*>(__builtin_assume_aligned(&Ls[lr + p], 16));
+        }
+        uint32_t s = __float_as_uint(Lg[p % 4]);
+        static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int e = col_edge<C>(j, decltype(kk)::value);
+            constexpr int r = edge_row<C>(e), t = e - edge_off<C>(r);
+            constexpr int sh = C::SHR[r][t];
+            msg[e] = rot(std::integral_constant<int, (sh == 0) ? 0 : Z - sh>{}, msg[e]);
+            s = padd(s, msg[e]);
+        });
+        return pmin(pmax(s, NAM), AM);
+    };
+    auto v2c_col = [&](auto jj, uint32_t ap) __attribute__((always_inline)) {
+        constexpr int j = decltype(jj)::value;
+        static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int e = col_edge<C>(j, decltype(kk)::value);
+            msg[e] = pmin(pmax(psub(ap, msg[e]), NQM), QM);
+        });
+    };
+
+    // early stop: codeword k of this wave = (group g, fp16 half p), k = 2g + p; converged ones park APP
+    constexpr uint64_t ACTIVE = lane_range_mask<Z, CPW>(0, Z);
+    constexpr uint64_t G0 = lane_range_mask<Z, 1>(0, Z), G1 = (CPW == 2) ? (G0 << 32) : 0;
+    constexpr uint32_t ALL = (CPW == 2) ? 0xfu : 0x3u;
+    uint32_t done = 0;  // bit k: codeword k converged
+    int used0 = iters, used1 = iters, used2 = iters, used3 = iters;
+    _Float16* Lh = reinterpret_cast<_Float16*>(Ls);
+
+    int it = 0;
+    for (; it + 1 < iters; ++it) {
+        cn_phase();
+        if constexpr (EARLY) {
+            uint32_t app[NB];
+            static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
+                constexpr int p = decltype(pp)::value;
+                app[lcol<C>(p)] = vn_col(pp);
+            });
+            // syndrome of APP_{it+1} per fp16 half k (one codeword per lane group each): per block column one
+            // ballot of the hard decisions (oracle: bit = APP < 0), rotated into each check's frame and XOR-ed
+            uint32_t conv = 0;  // bit 2g + k: group g's codeword k satisfies every check
+            static_for<0, 2>([&](auto kk) __attribute__((always_inline)) {
+                constexpr int k = decltype(kk)::value;
+                uint64_t par[MB];
+#pragma unroll
+                for (int r = 0; r < MB; ++r) par[r] = 0;
+                static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                    constexpr int j = decltype(jj)::value;
+                    const uint64_t b = __ballot(as_h2(app[j])[k] < (_Float16)0) & ACTIVE;
+                    static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                        constexpr int r = decltype(rr)::value;
+                        constexpr int t = first_slot<C>(r, j);
+                        if constexpr (t >= 0) par[r] ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                    });
+                });
+                uint64_t u = 0;
+#pragma unroll
+                for (int r = 0; r < MB; ++r) u |= par[r];
+                conv |= ((u & G0) ? 0u : 1u) << k;
+                if constexpr (CPW == 2) conv |= ((u & G1) ? 0u : 1u) << (2 + k);
+            });
+            const uint32_t fresh = conv & ~done;
+            if (fresh) {
+                if (fresh & 1u) used0 = it + 1;
+                if (fresh & 2u) used1 = it + 1;
+                if (fresh & 4u) used2 = it + 1;
+                if (fresh & 8u) used3 = it + 1;
+                // park APP of a newly converged codeword in its fp16 half of the L row (L no longer needed)
+                const int g = (CPW == 2) ? half : 0;
+                const bool park0 = (fresh >> (2 * g)) & 1u, park1 = (fresh >> (2 * g + 1)) & 1u;
+                if (park0 || park1) {
+                    static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                        constexpr int j = decltype(jj)::value;
+                        const h2 hv = as_h2(app[j]);
+                        if (park0) Lh[2 * (lrow + lpos<C>(j))] = hv[0];
+                        if (park1) Lh[2 * (lrow + lpos<C>(j)) + 1] = hv[1];
+                    });
+                }
+                done |= fresh;
+                if (done == ALL) break;
+            }
+            static_for<0, NB>([&](auto jj) __attribute__((always_inline)) { v2c_col(jj, app[decltype(jj)::value]); });
+        } else {
+            static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
+                constexpr int p = decltype(pp)::value;
+                v2c_col(std::integral_constant<int, lcol<C>(p)>{}, vn_col(pp));
+            });
+        }
+    }
+    // last iteration (or early exit): outputs straight from the VN phase
+    const bool early_exit = EARLY && done == ALL;
+    if (!early_exit && iters > 0) cn_phase();
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int zo = (CPW == 2) ? (tid & 31) : (tid & 63);
+    const int go = (CPW == 2) ? ((tid >> 5) & 1) : 0;
+    const int64_t c0 = ((((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + go) * 2;
+    const bool park0 = EARLY && ((done >> (2 * go)) & 1u), park1 = EARLY && ((done >> (2 * go + 1)) & 1u);
+    const bool ok0 = zo < Z && c0 < B, ok1 = zo < Z && c0 + 1 < B;
+    static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
+        constexpr int p = decltype(pp)::value;
+        constexpr int j = lcol<C>(p);
+        uint32_t ap;
+        if (iters > 0 && !early_exit) ap = vn_col(pp);
+        else ap = pmin(pmax(Ls[lrow + p], NAM), AM);  // iters == 0: APP_0; early exit: parked (already sat)
+        h2 hv = as_h2(ap);
+        if (park0) hv[0] = Lh[2 * (lrow + p)];
+        if (park1) hv[1] = Lh[2 * (lrow + p) + 1];
+        int t = zo + C::PHI[j];
+        t -= (t >= Z) ? Z : 0;
+        const int64_t o = (int64_t)j * Z + t;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (k == 0 ? ok0 : ok1) {
+                const int64_t oo = (c0 + k) * N + o;
+                const float zz = 0.5f * (float)hv[k];
+                if (bits) bits[oo] = (uint8_t)(zz <= kZthrF32);
+                if (soft) soft[oo] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + expf(-zz));
+            }
+        }
+    });
+    if (zo == 0 && iters_used) {
+        if (ok0) iters_used[c0] = go ? used2 : used0;
+        if (ok1) iters_used[c0 + 1] = go ? used3 : used1;
+    }
+}
+
+template <class C>
+static int launch_qms_pk(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
+                         hipStream_t st) {
+    constexpr int CPW = (C::Z <= 32) ? 2 : 1;
+    const int64_t waves = (B + 2 * CPW - 1) / (2 * CPW);
+    const unsigned blocks = (unsigned)((waves + QC_PK_TPB / 64 - 1) / (QC_PK_TPB / 64));
+    const float qm = (float)p.qmax, am = (float)p.app_max, b = p.beta, qi = 1.0f / p.qstep;
+    const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
+    const float* x = (const float*)llr;
+    float* sf = (float*)soft;
+#define PK(E, BT) k_qc_qms_pk<C, E, BT><<<blocks, QC_PK_TPB, 0, st>>>(x, B, p.iters, qm, am, b, qi, p.flags, bits, sf, used)
+    if (b != 0.0f) {
+        if (es) PK(true, true); else PK(false, true);
+    } else {
+        if (es) PK(true, false); else PK(false, false);
+    }
+#undef PK
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(LDPC_EHIP, "qc packed kernel launch: %s", hipGetErrorString(e));
+    return LDPC_OK;
+}
+
+int qc_launch_qms_pk_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                                int32_t* used, hipStream_t st) {
+    return launch_qms_pk<Wifi648_12>(llr, B, p, bits, soft, used, st);
+}
+int qc_launch_qms_pk_wifi1296_23(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                                 int32_t* used, hipStream_t st) {
+    return launch_qms_pk<Wifi1296_23>(llr, B, p, bits, soft, used, st);
+}
+
+}  // namespace ldpc

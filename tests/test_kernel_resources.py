@@ -1,0 +1,54 @@
+"""Every kernel a BASELINE.json configuration dispatches is spill-free: no VGPR spills and no scratch, read
+from the gfx950 code objects' AMDGPU metadata notes of the built libldpc_hip.so (no GPU needed;
+scripts/kernel_resources.py).  SGPR spills go to VGPR lanes (v_writelane), not to memory, and are allowed.
+
+    [1] (648,1/2) min-sum 50 it          k_qc_ms_ph<Wifi648_12, false, false, 0>
+    [2] (1944,5/6) tanh-SP, 16-QAM OFDM   k_qc_sp_sl<Wifi1944_56>
+    [3] (1296,2/3) 5-bit min-sum 20 it ES k_qc_qms_pk<Wifi1296_23, *, *>  (packed fp16, two codewords per lane)
+    [4] DVB-S2 64800 rate 1/2, 50 it      generic CSR kernels at degree bound 8 (k_vn_ms/k_cn_ms, k_vn_sp/k_cn_sp),
+                                          k_load_llr, k_final
+    drop-in decode_bits on (648,1/2)      k_qc_sp_st<Wifi648_12, false>
+"""
+import os
+import re
+import shutil
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+BASELINE_KERNELS = [
+    r"k_qc_ms_ph<ldpc::Wifi648_12, false, false, 0>",
+    r"k_qc_sp_sl<ldpc::Wifi1944_56>",
+    r"k_qc_qms_pk<ldpc::Wifi1296_23, (true|false), (true|false)>",
+    r"k_vn_ms<8, (true|false), \d>",
+    r"k_cn_ms<8, (true|false), \d>",
+    r"k_vn_sp<float, 8, false, \d>",
+    r"k_cn_sp<float, 8, false, \d>",
+    r"k_load_llr<float, true>",
+    r"k_final<float, 32, (true|false)>",
+    r"k_qc_sp_st<ldpc::Wifi648_12, false>",
+]
+
+
+@pytest.fixture(scope="module")
+def resources():
+    import kernel_resources as kr
+    if not os.path.exists(kr.READELF) or not shutil.which("c++filt"):
+        pytest.skip("llvm-readelf / c++filt not available")
+    if not os.path.exists(kr.DEFAULT_LIB):
+        pytest.fail("libldpc_hip.so is not built")
+    ks = kr.kernels()
+    names = sorted(ks)
+    return {d: ks[n] for n, d in zip(names, kr.demangle(names))}
+
+
+@pytest.mark.parametrize("pattern", BASELINE_KERNELS)
+def test_baseline_config_kernels_do_not_spill(resources, pattern):
+    hits = {d: r for d, r in resources.items() if re.search(r"ldpc::" + pattern, d)}
+    assert hits, f"no kernel matches {pattern}"
+    for d, r in hits.items():
+        assert r.get("vgpr_spill_count", 0) == 0, (d, r)
+        assert r.get("private_segment_fixed_size", 0) == 0, (d, r)

@@ -427,7 +427,8 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
             // sign of the product folded into the two magnitudes once per row
             const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);
             const float M2 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn2, alpha, beta, clamp)) ^ tot);
-            // NORM_PLAIN: compare-free select as in k_qc_ms_ph (med3 of the unsigned magnitudes, XOR)
+            // NORM_PLAIN: compare-free select (med3 of the unsigned magnitudes, XOR): +3.4 % on (1296,2/3), A/B;
+            // -1.3 % in the LDS-bound k_qc_ms_ph, which keeps v_cmp/v_cndmask
             const float A1 = mag_of<NORM>(mn1, alpha, beta, clamp), A2 = mag_of<NORM>(mn2, alpha, beta, clamp);
             const uint32_t X = __float_as_uint(M1) ^ __float_as_uint(A2);
 #if !QC_L128
@@ -519,12 +520,6 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #endif
 #ifndef QC_PH_WAVES_PER_SIMD
 #define QC_PH_WAVES_PER_SIMD 4
-#endif
-#ifndef QC_PH_SKEW
-#define QC_PH_SKEW 0
-#endif
-#ifndef QC_PH_SCHED
-#define QC_PH_SCHED 0  // > 0: interleave one LDS op per QC_PH_SCHED VALU in the loop (sched_group_barrier)
 #endif
 #ifndef QC_PH_WAVES_PER_SIMD_EARLY
 #define QC_PH_WAVES_PER_SIMD_EARLY 3  // spill-free (145 VGPRs): 648 min-sum early stop 24.6 -> 57.9 M cw/s (A/B)
@@ -661,10 +656,6 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         });
     };
 
-#if QC_PH_SKEW
-    // A/B: desynchronise the waves sharing a CU's LDS pipe (odd waves start about half an iteration late)
-    if ((threadIdx.x >> 6) & 1) __builtin_amdgcn_s_sleep(QC_PH_SKEW);
-#endif
     int it = 0;
     for (; it + 1 < iters; ++it) {
         cn_phase();
@@ -710,14 +701,6 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
                 constexpr int p = decltype(pp)::value;
                 v2c_col(std::integral_constant<int, lcol<C>(p)>{}, vn_col(pp));
             });
-#if QC_PH_SCHED
-            // scheduling hint (A/B): spread the LDS rotations evenly through the VALU stream instead of
-            // bursts of one row's gathers, so a wave rarely stalls on a full LDS queue
-            static_for<0, 100>([&](auto) __attribute__((always_inline)) {
-                __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);           // one DS instruction
-                __builtin_amdgcn_sched_group_barrier(0x002, QC_PH_SCHED, 0); // then N VALU
-            });
-#endif
         }
     }
     // last iteration (or early exit): outputs straight from the VN phase, column by column

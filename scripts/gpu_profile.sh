@@ -9,7 +9,7 @@ set -o pipefail
 OUT=${OUT:-gpurun_out}; mkdir -p $OUT; export TMPDIR=/tmp
 NAME=${NAME:-headline}
 KERNEL=${KERNEL:-k_qc_ms}
-ARGS=${ARGS:-}
+ARGS="${ARGS:-} --no-dropin"  # the drop-in / tanh-SP side measurements are not profiled
 PARGS=${PARGS:---steps 4 --warmup 1}
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
 P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE"
@@ -23,3 +23,4 @@ for grp in "$P1" "$P2" FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d $D/pmc$i -o run -- python3 bench.py $ARGS $PARGS --no-cpu-baseline > $D/pmc$i.json 2> $D/pmc$i.err || { echo "pmc pass $i ($NAME) failed"; tail -5 $D/pmc$i.err; exit 1; }
 done
 python3 scripts/counters_summary.py $D --name $NAME --kernel "$KERNEL" > $OUT/counters_$NAME.json && echo "counters_$NAME.json written"
+python3 scripts/timed_launches.py $D --kernel "$KERNEL" > $D/timed.json 2>/dev/null || true

@@ -1027,7 +1027,7 @@ int qc_z(const QCSpec* s) { return s ? s->z : 0; }
 bool qc_supports(const QCSpec* s, const ldpc_params& p) {
     if (!s) return false;
     if (p.flags & LDPC_F_F64) return false;
-    if (p.algo == LDPC_ALGO_TANH_SP) return s->z <= 64 || !(p.flags & LDPC_F_EARLY_STOP);  // sliced tanh-SP: fixed iterations
+    if (p.algo == LDPC_ALGO_TANH_SP) return true;  // Z <= 64: k_qc_sp_st; Z = 81: k_qc_sp_sl (both with early stop)
     return p.algo == LDPC_ALGO_MIN_SUM || p.algo == LDPC_ALGO_QMIN_SUM;
 }
 

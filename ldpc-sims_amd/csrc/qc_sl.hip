@@ -1,7 +1,5 @@
 // qc_sl.hip — sliced register kernels for quasi-cyclic codes with Z > 64 (802.11n Z = 81), gfx950.
-#include "qc_common.h"
-
-namespace ldpc {
+#include "qc_sl_sp.h"
 
 // ---- sliced register kernels for Z > 64 (802.11n Z = 81) -----------------------------------------
 // The lifting index is split into S slots of ZL = Z / S <= 32 lanes: a unit of S waves decodes two
@@ -12,146 +10,9 @@ namespace ldpc {
 // and the reader loads position zc + rho — one base VGPR per lane, every offset an instruction
 // immediate.  Rotation-0 circulants (the lane frames make 30 of 79 so for (1944,5/6)) stay in registers.
 // Per block row: store v2c, barrier, gather, check update, store c2v, barrier, scatter (two buffers).
-template <class C>
-constexpr int nz_count(int r) {  // circulants of row r with a nonzero rotation
-    int c = 0;
-    for (int t = 0; t < C::DEG[r]; ++t) c += (C::SHR[r][t] != 0);
-    return c;
-}
-template <class C>
-constexpr int nz_index(int r, int t) {
-    int c = 0;
-    for (int u = 0; u < t; ++u) c += (C::SHR[r][u] != 0);
-    return c;
-}
-template <class C>
-constexpr int nz_max() {
-    int m = 1;
-    for (int r = 0; r < C::MB; ++r) m = nz_count<C>(r) > m ? nz_count<C>(r) : m;
-    return m;
-}
+// The tanh-SP kernel and the shared helpers are in qc_sl_sp.h.
 
-#ifndef QC_SL_WAVES_PER_SIMD
-#define QC_SL_WAVES_PER_SIMD 3
-#endif
-#ifndef QC_SL_SP_WAVES_PER_SIMD
-#define QC_SL_SP_WAVES_PER_SIMD 2  // spill-free (3 waves: 83 VGPRs spilled), same speed (1.446 vs 1.448 M cw/s)
-#endif
-
-template <class C>
-__global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_SL_SP_WAVES_PER_SIMD)))
-void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
-                uint8_t* __restrict__ bits, float* __restrict__ soft) {
-    constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
-    constexpr int NE = edge_off<C>(MB), NT = nz_max<C>(), ROW = 2 * 2 * Z;  // floats per exchanged circulant
-    static_assert(S > 1 && Z % S == 0 && ZL <= 32, "sliced kernel: Z = S * ZL, ZL <= 32");
-    __shared__ float Xv[NT * ROW], Xc[NT * ROW];
-    const int k = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // slot of this wave
-    const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
-    const int64_t cw = (int64_t)blockIdx.x * 2 + h;
-    const bool live = l < ZL;                // lane carries a frame position
-    const bool valid = live && cw < B;       // ... of a real codeword
-    const int zc = live ? l + ZL * k : 0;    // idle lanes alias position 0 for reads (never store)
-    const int xb = h * 2 * Z + zc;           // this lane's position in an exchange row
-    // L = -llr (bp.py:47) of this lane's variable in every block column, kept in VGPRs
-    float Lr[NB];
-    {
-        const int64_t base = valid ? cw * N : 0;
-        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-            constexpr int j = decltype(jj)::value;
-            int t = zc + C::PHI[j];
-            t -= (t >= Z) ? Z : 0;
-            Lr[j] = valid ? -llr[base + j * Z + t] : 0.0f;
-        });
-    }
-    float msg[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
-
-    for (int it = 0; it < iters; ++it) {
-        // VC + tanh in the variable frame (as k_qc_sp_st)
-        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-            constexpr int j = decltype(jj)::value;
-            constexpr int dj = col_deg<C>(j);
-            float P = 0.0f;
-            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
-                constexpr int q = decltype(kk)::value;
-                constexpr int e = col_edge<C>(j, q);
-                float Ssum = P;
-                static_for<q + 1, dj>([&](auto uu) __attribute__((always_inline)) {
-                    Ssum += msg[col_edge<C>(j, decltype(uu)::value)];
-                });
-                const float v = Num<float>::tanh_(0.5f * (Lr[j] + Ssum));
-                P += msg[e];
-                msg[e] = v;
-            });
-        });
-        // CV per block row through the LDS exchange
-        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
-            constexpr int r = decltype(rr)::value;
-            constexpr int d = C::DEG[r];
-            constexpr int e0 = edge_off<C>(r);
-            if (live) {
-                static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                    constexpr int t = decltype(tt)::value;
-                    if constexpr (C::SHR[r][t] != 0) {
-                        constexpr int o = nz_index<C>(r, t) * ROW;
-                        Xv[o + xb] = msg[e0 + t];
-                        Xv[o + xb + Z] = msg[e0 + t];
-                    }
-                });
-            }
-            __syncthreads();
-            float g[d];
-            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                constexpr int t = decltype(tt)::value;
-                constexpr int s = C::SHR[r][t];
-                if constexpr (s == 0) g[t] = msg[e0 + t];
-                else g[t] = Xv[nz_index<C>(r, t) * ROW + xb + s];
-            });
-            float Q = 1.0f;
-            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                constexpr int t = decltype(tt)::value;
-                float p = Q;
-                static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
-                Q *= g[t];
-                const float y = cn_tanh_out(p, clamp);
-                g[t] = y;  // g[t] is not read again (products use u > t)
-            });
-            if (live) {
-                static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                    constexpr int t = decltype(tt)::value;
-                    if constexpr (C::SHR[r][t] != 0) {
-                        constexpr int o = nz_index<C>(r, t) * ROW;
-                        Xc[o + xb] = g[t];
-                        Xc[o + xb + Z] = g[t];
-                    }
-                });
-            }
-            __syncthreads();
-            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                constexpr int t = decltype(tt)::value;
-                constexpr int s = C::SHR[r][t];
-                if constexpr (s == 0) msg[e0 + t] = g[t];
-                else msg[e0 + t] = Xc[nz_index<C>(r, t) * ROW + xb + (Z - s)];
-            });
-        });
-    }
-    if (valid) {
-        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-            constexpr int j = decltype(jj)::value;
-            constexpr int dj = col_deg<C>(j);
-            float Ssum = 0.0f;
-            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) { Ssum += msg[col_edge<C>(j, decltype(kk)::value)]; });
-            const float zz = 0.5f * (Lr[j] + Ssum);
-            int t = zc + C::PHI[j];
-            t -= (t >= Z) ? Z : 0;
-            const int64_t o = cw * N + j * Z + t;
-            if (bits) bits[o] = (uint8_t)Num<float>::bit(zz);
-            if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
-        });
-    }
-}
+namespace ldpc {
 
 // Min-sum, stored messages in the CHECK frame (fixed iterations or early stop, float or 5-bit quantized).
 // Per iteration: every wave publishes APP_it of its slot (two copies per position) to LDS, one barrier;
@@ -304,6 +165,9 @@ void k_qc_ms_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     }
 }
 
+int qc_launch_sp_sl_es_wifi1944_56(const float* llr, int64_t B, const ldpc_params& p, uint8_t* bits, float* soft,
+                                   int32_t* used, hipStream_t st);
+
 template <class C>
 static int launch_sl(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
                      hipStream_t st) {
@@ -312,9 +176,13 @@ static int launch_sl(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
     const float* x = (const float*)llr;
     float* sf = (float*)soft;
-    if (p.algo == LDPC_ALGO_TANH_SP) {  // qc_supports: fixed iteration count only
-        k_qc_sp_sl<C><<<blocks, tb, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf);
-        if (used) fill_i32(used, B, p.iters, st);
+    if (p.algo == LDPC_ALGO_TANH_SP) {
+        if (es) {
+            static_assert(std::is_same_v<C, Wifi1944_56>, "one sliced code");
+            qc_launch_sp_sl_es_wifi1944_56(x, B, p, bits, sf, used, st);
+        } else {
+            k_qc_sp_sl<C, false><<<blocks, tb, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+        }
     } else if (p.algo == LDPC_ALGO_QMIN_SUM) {
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;
 #define QL(E, N) k_qc_ms_sl<C, true, E, N><<<blocks, tb, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used)

@@ -1,0 +1,15 @@
+// qc_sl_es.hip — tanh-SP with early termination on the sliced Z = 81 kernel (qc_sl_sp.h), built with the
+// default (max-occupancy) scheduler: 2 waves/SIMD without scratch (build.py PER_FILE).
+#include "qc_sl_sp.h"
+
+namespace ldpc {
+
+int qc_launch_sp_sl_es_wifi1944_56(const float* llr, int64_t B, const ldpc_params& p, uint8_t* bits, float* soft,
+                                   int32_t* used, hipStream_t st) {
+    using C = Wifi1944_56;
+    k_qc_sp_sl<C, true><<<(unsigned)((B + 1) / 2), dim3(C::S * 64), 0, st>>>(llr, B, p.iters, p.clamp, p.flags, bits,
+                                                                             soft, used);
+    return LDPC_OK;
+}
+
+}  // namespace ldpc

@@ -1,0 +1,270 @@
+// qc_sl_sp.h — the sliced tanh-SP kernel for Z > 64 (802.11n Z = 81) and the sliced kernels' helpers.
+// Included by qc_sl.hip (fixed iteration count, iterative-ILP scheduler) and qc_sl_es.hip (early stop,
+// default scheduler: with the ILP scheduler the early-stop variant needs > 256 VGPRs and spills).
+#pragma once
+#include "qc_common.h"
+
+namespace ldpc {
+
+template <class C>
+constexpr int nz_count(int r) {  // circulants of row r with a nonzero rotation
+    int c = 0;
+    for (int t = 0; t < C::DEG[r]; ++t) c += (C::SHR[r][t] != 0);
+    return c;
+}
+template <class C>
+constexpr int nz_index(int r, int t) {
+    int c = 0;
+    for (int u = 0; u < t; ++u) c += (C::SHR[r][u] != 0);
+    return c;
+}
+template <class C>
+constexpr int nz_max() {
+    int m = 1;
+    for (int r = 0; r < C::MB; ++r) m = nz_count<C>(r) > m ? nz_count<C>(r) : m;
+    return m;
+}
+
+#ifndef QC_SL_WAVES_PER_SIMD
+#define QC_SL_WAVES_PER_SIMD 3
+#endif
+#ifndef QC_SL_SP_WAVES_PER_SIMD
+#define QC_SL_SP_WAVES_PER_SIMD 2  // spill-free (3 waves: 83 VGPRs spilled), same speed (1.446 vs 1.448 M cw/s)
+#endif
+
+// Early stop (EARLY): before iteration it >= 1, every lane sums its columns' c2v (ascending, the generic VN
+// kernel's operations) into z_it = 0.5 * (L + sum) and publishes the hard decision to LDS (two copies per
+// position, like the exchange rows); each check lane then XORs the decisions of its edges' variables (the
+// gather's positions) and the unit's waves pool one ballot per (slot, codeword) in LDS.  A codeword whose
+// syndrome is zero writes its outputs from z_it right there (iters_used = it) and is skipped at the end;
+// the unit leaves the loop when both of its codewords are done.  Bitwise equal to the generic path.
+// QC_SL_SP_COMPACT: L in LDS (not VGPRs) and one exchange buffer for v2c and c2v (a third barrier per
+// row instead of a second buffer): 41 instead of 52 KB of LDS and 24 fewer VGPRs per workgroup, so three
+// units fit a CU at 3 waves/SIMD without scratch.
+#ifndef QC_SL_SP_COMPACT
+#define QC_SL_SP_COMPACT 0  // A/B: 1.51 vs 1.45 M cw/s at 3 waves/SIMD but 19 VGPRs spilled; 1.30 at 2 waves
+#endif
+
+template <class C, bool EARLY>
+__global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_SL_SP_WAVES_PER_SIMD)))
+void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
+                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
+    constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
+    constexpr int NE = edge_off<C>(MB), NT = nz_max<C>(), ROW = 2 * 2 * Z;  // floats per exchanged circulant
+    static_assert(S > 1 && Z % S == 0 && ZL <= 32, "sliced kernel: Z = S * ZL, ZL <= 32");
+#if QC_SL_SP_COMPACT
+    __shared__ float Xv[NT * ROW];
+    float* const Xc = Xv;
+    __shared__ float Lsh[2 * NB * Z];  // L of both codewords: [half][j][position]
+#else
+    __shared__ float Xv[NT * ROW], Xc[NT * ROW];
+#endif
+    const int k = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // slot of this wave
+    const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
+    const int64_t cw = (int64_t)blockIdx.x * 2 + h;
+    const bool live = l < ZL;                // lane carries a frame position
+    const bool valid = live && cw < B;       // ... of a real codeword
+    const int zc = live ? l + ZL * k : 0;    // idle lanes alias position 0 for reads (never store)
+    const int xb = h * 2 * Z + zc;           // this lane's position in an exchange row
+    // L = -llr (bp.py:47) of this lane's variable in every block column
+#if QC_SL_SP_COMPACT
+    const int lb = h * NB * Z + zc;
+    auto Lr_at = [&](int j) __attribute__((always_inline)) {
+        int a = lb;
+        asm volatile("" : "+v"(a));  // re-read every iteration, not hoisted into registers
+        return Lsh[a + j * Z];
+    };
+    {
+        const int64_t base = valid ? cw * N : 0;
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            int t = zc + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            const float x = valid ? -llr[base + j * Z + t] : 0.0f;
+            if (live) Lsh[lb + j * Z] = x;
+        });
+    }
+    __syncthreads();
+#else
+    float Lr[NB];
+    auto Lr_at = [&](int j) __attribute__((always_inline)) { return Lr[j]; };
+    {
+        const int64_t base = valid ? cw * N : 0;
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            int t = zc + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            Lr[j] = valid ? -llr[base + j * Z + t] : 0.0f;
+        });
+    }
+#endif
+    float msg[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
+    // outputs of this lane's codeword from z of every column (end of the loop, or at convergence)
+    auto emit = [&](auto zfun) __attribute__((always_inline)) {
+        if (valid) {
+            static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                constexpr int j = decltype(jj)::value;
+                const float zz = zfun(jj);
+                int t = zc + C::PHI[j];
+                t -= (t >= Z) ? Z : 0;
+                const int64_t o = cw * N + j * Z + t;
+                if (bits) bits[o] = (uint8_t)Num<float>::bit(zz);
+                if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
+            });
+        }
+    };
+    auto zsum = [&](auto jj) __attribute__((always_inline)) {  // z = 0.5 * (L + ascending sum of c2v)
+        constexpr int j = decltype(jj)::value;
+        float Ssum = 0.0f;
+        static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) { Ssum += msg[col_edge<C>(j, decltype(kk)::value)]; });
+        return 0.5f * (Lr_at(j) + Ssum);
+    };
+    constexpr int HROW = 2 * 2 * Z;  // hard decisions: [j][half][2Z] bytes
+    __shared__ uint8_t Hb[EARLY ? NB * HROW : 1];
+    __shared__ uint32_t Fl[2 * S];
+    __shared__ float Zp[EARLY ? 2 * NB * Z : 1];  // parked z of converged codewords, [half][j][position]
+    const int64_t cwp = (int64_t)blockIdx.x * 2;
+    bool done0 = cwp >= B, done1 = cwp + 1 >= B;  // a missing codeword counts as converged
+    int used0 = iters, used1 = iters;
+
+    for (int it = 0; it < iters; ++it) {
+        if constexpr (EARLY) {
+            if (it > 0) {
+                if (live) {
+                    static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                        constexpr int j = decltype(jj)::value;
+                        const uint8_t b = (uint8_t)Num<float>::bit(zsum(jj));
+                        Hb[j * HROW + xb] = b;
+                        Hb[j * HROW + xb + Z] = b;
+                    });
+                }
+                __syncthreads();
+                uint32_t un = 0;  // some check of this lane's codeword position is unsatisfied
+                static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                    constexpr int r = decltype(rr)::value;
+                    uint32_t par = 0;
+                    static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                        constexpr int t = decltype(tt)::value;
+                        par ^= Hb[C::COL[r][t] * HROW + xb + C::SHR[r][t]];
+                    });
+                    un |= par;
+                    asm volatile("" : "+v"(un));  // one row's loads in flight at a time (register budget)
+                });
+                const uint64_t bu = __ballot(live && un != 0);
+                if (lane == 0) {
+                    Fl[2 * k] = (uint32_t)((bu & 0xffffffffull) != 0);
+                    Fl[2 * k + 1] = (uint32_t)((bu >> 32) != 0);
+                }
+                __syncthreads();
+                uint32_t u0 = 0, u1 = 0;
+#pragma unroll
+                for (int q = 0; q < S; ++q) {
+                    u0 |= Fl[2 * q];
+                    u1 |= Fl[2 * q + 1];
+                }
+                const bool new0 = !done0 && u0 == 0, new1 = !done1 && u1 == 0;
+                if (new0) used0 = it;
+                if (new1) used1 = it;
+                if (live && (h ? new1 : new0)) {  // park z_it, this codeword's output (emitted after the loop)
+                    static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                        constexpr int j = decltype(jj)::value;
+                        float Ssum = 0.0f;
+                        asm volatile("" : "+v"(Ssum));  // not CSE'd with the syndrome pass above
+                        static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) {
+                            Ssum += msg[col_edge<C>(j, decltype(kk)::value)];
+                        });
+                        Zp[(h * NB + j) * Z + zc] = 0.5f * (Lr_at(j) + Ssum);
+                    });
+                }
+                done0 |= new0;
+                done1 |= new1;
+                if (done0 && done1) break;
+                // (Hb / Fl are rewritten only after this iteration's row barriers: no barrier needed here)
+            }
+        }
+        // VC + tanh in the variable frame (as k_qc_sp_st)
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            constexpr int dj = col_deg<C>(j);
+            const float Lj = Lr_at(j);
+            float P = 0.0f;
+            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
+                constexpr int q = decltype(kk)::value;
+                constexpr int e = col_edge<C>(j, q);
+                float Ssum = P;
+                static_for<q + 1, dj>([&](auto uu) __attribute__((always_inline)) {
+                    Ssum += msg[col_edge<C>(j, decltype(uu)::value)];
+                });
+                const float v = Num<float>::tanh_(0.5f * (Lj + Ssum));
+                P += msg[e];
+                msg[e] = v;
+            });
+        });
+        // CV per block row through the LDS exchange
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            constexpr int d = C::DEG[r];
+            constexpr int e0 = edge_off<C>(r);
+            if (live) {
+                static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                    constexpr int t = decltype(tt)::value;
+                    if constexpr (C::SHR[r][t] != 0) {
+                        constexpr int o = nz_index<C>(r, t) * ROW;
+                        Xv[o + xb] = msg[e0 + t];
+                        Xv[o + xb + Z] = msg[e0 + t];
+                    }
+                });
+            }
+            __syncthreads();
+            float g[d];
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int s = C::SHR[r][t];
+                if constexpr (s == 0) g[t] = msg[e0 + t];
+                else g[t] = Xv[nz_index<C>(r, t) * ROW + xb + s];
+            });
+            float Q = 1.0f;
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                float p = Q;
+                static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
+                Q *= g[t];
+                const float y = cn_tanh_out(p, clamp);
+                g[t] = y;  // g[t] is not read again (products use u > t)
+            });
+#if QC_SL_SP_COMPACT
+            __syncthreads();  // every wave has read this row's v2c before the buffer takes its c2v
+#endif
+            if (live) {
+                static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                    constexpr int t = decltype(tt)::value;
+                    if constexpr (C::SHR[r][t] != 0) {
+                        constexpr int o = nz_index<C>(r, t) * ROW;
+                        Xc[o + xb] = g[t];
+                        Xc[o + xb + Z] = g[t];
+                    }
+                });
+            }
+            __syncthreads();
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int s = C::SHR[r][t];
+                if constexpr (s == 0) msg[e0 + t] = g[t];
+                else msg[e0 + t] = Xc[nz_index<C>(r, t) * ROW + xb + (Z - s)];
+            });
+#if QC_SL_SP_COMPACT
+            __syncthreads();  // ... and its c2v before the next row's v2c lands in the buffer
+#endif
+        });
+    }
+    if (EARLY && (h ? done1 : done0)) {
+        emit([&](auto jj) __attribute__((always_inline)) { return Zp[(h * NB + decltype(jj)::value) * Z + zc]; });
+    } else {
+        emit(zsum);
+    }
+    if (valid && k == 0 && l == 0 && iters_used) iters_used[cw] = h ? used1 : used0;
+}
+
+}  // namespace ldpc

@@ -334,15 +334,16 @@ def test_qc_sp_equals_generic_sp_bitwise(code, B):
     assert bool((r["iters_used"] == 30).all())
 
 
-@pytest.mark.parametrize("code", ["wifi648_12", "wifi1296_23"])
+@pytest.mark.parametrize("code", ["wifi648_12", "wifi1296_23", "wifi1944_56"])
 @pytest.mark.parametrize("B", [1, 2, 777])
 def test_qc_sp_early_stop_equals_generic_bitwise(code, B):
-    """tanh-SP with early termination in the register kernel: iteration counts, bits and z equal the
-    generic kernels' (whose counts equal the oracle's, test_generic_early_stop_vs_oracle), including
-    codeword pairs of one wave that stop at different iterations and an odd batch."""
+    """tanh-SP with early termination in the register kernels (Z <= 64: k_qc_sp_st; Z = 81: the sliced
+    k_qc_sp_sl, whose three waves agree through LDS): iteration counts, bits and z equal the generic
+    kernels' (whose counts equal the oracle's, test_generic_early_stop_vs_oracle), including codeword pairs
+    that stop at different iterations and an odd batch."""
     H, qc = get_code(code)
     rate = 1 - H.shape[0] / H.shape[1]
-    cw, llr = _llr(H, B, 2.0 if rate < 0.6 else 3.5, seed=51 + B, rate=rate)
+    cw, llr = _llr(H, B, 2.0 if rate < 0.6 else (3.5 if rate < 0.8 else 4.2), seed=51 + B, rate=rate)
     if B > 2:
         llr[2] = np.float32(-50.0) * (1 - 2 * cw[2])     # converges at the first check
     dec = ldpc_amd.get_decoder(H)
@@ -433,3 +434,34 @@ def test_quantized_minsum_rejects_fractional_offset_and_alpha():
         with pytest.raises(_abi.LdpcError):
             dec.decode(x, 3, algo="qminsum", **kw)
     dec.decode(x, 3, algo="qminsum", beta=1.0)
+
+
+@pytest.mark.parametrize("code", ["wifi648_12", "wifi1296_23"])
+@pytest.mark.parametrize("B", [1, 2, 3, 5, 127])
+@pytest.mark.parametrize("early", [False, True])
+def test_packed_quantized_ragged_batches(code, B, early):
+    """The packed 5-bit kernel holds 2 codewords per lane (4 per wave at Z = 27, 2 at Z = 54): batches that do
+    not fill the last lane group, its high fp16 half, or the last wave must decode exactly like the oracle
+    (bits, z, iteration counts) and write nothing past row B - 1."""
+    H, _ = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, B, 2.5 if rate < 0.6 else 4.0, seed=300 + B, rate=rate)
+    q = np.clip(np.rint(llr), -15, 15).astype(np.int8)
+    dec = ldpc_amd.get_decoder(H)
+    x = torch.from_numpy(llr).cuda()
+    r = dec.decode(x, 20, algo="qminsum", qmax=15, app_max=127, qstep=1.0, early_stop=early, soft="z", want_iters=True)
+    ref = oracle.qms(H, q, 20, 15, 127, 0, early_stop=early)
+    assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])
+    assert np.array_equal(r["soft"].cpu().numpy(), (0.5 * ref["app"]).astype(np.float32))
+    assert np.array_equal(r["iters_used"].cpu().numpy(), ref["iters_used"])
+    # no writes past the batch: decode into a larger buffer through the ABI and check the guard rows
+    p = dec.params(20, "qminsum", 15.0, 1.0, 0.0, early, "f32", "z", device_ptrs=True)
+    bits = torch.full((B + 4, H.shape[1]), 7, dtype=torch.uint8, device="cuda")
+    soft = torch.full((B + 4, H.shape[1]), 7.0, dtype=torch.float32, device="cuda")
+    used = torch.full((B + 4,), 77, dtype=torch.int32, device="cuda")
+    ws = torch.empty((max(dec.workspace_bytes(B, p), 1),), dtype=torch.uint8, device="cuda")
+    _abi.check(dec.lib.ldpc_decode_ex(dec._h, x.data_ptr(), B, p, bits.data_ptr(), soft.data_ptr(), used.data_ptr(),
+                                      ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert (bits[B:] == 7).all() and (soft[B:] == 7.0).all() and (used[B:] == 77).all()
+    assert np.array_equal(bits[:B].cpu().numpy(), ref["bits"])

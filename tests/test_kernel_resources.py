@@ -3,7 +3,7 @@ from the gfx950 code objects' AMDGPU metadata notes of the built libldpc_hip.so 
 scripts/kernel_resources.py).  SGPR spills go to VGPR lanes (v_writelane), not to memory, and are allowed.
 
     [1] (648,1/2) min-sum 50 it          k_qc_ms_ph<Wifi648_12, false, false, 0>
-    [2] (1944,5/6) tanh-SP, 16-QAM OFDM   k_qc_sp_sl<Wifi1944_56>
+    [2] (1944,5/6) tanh-SP, 16-QAM OFDM   k_qc_sp_sl<Wifi1944_56, *> (fixed; early stop too)
     [3] (1296,2/3) 5-bit min-sum 20 it ES k_qc_qms_pk<Wifi1296_23, *, *>  (packed fp16, two codewords per lane)
     [4] DVB-S2 64800 rate 1/2, 50 it      generic CSR kernels at degree bound 8 (k_vn_ms/k_cn_ms, k_vn_sp/k_cn_sp),
                                           k_load_llr, k_final
@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 BASELINE_KERNELS = [
     r"k_qc_ms_ph<ldpc::Wifi648_12, false, false, 0>",
-    r"k_qc_sp_sl<ldpc::Wifi1944_56>",
+    r"k_qc_sp_sl<ldpc::Wifi1944_56, (true|false)>",
     r"k_qc_qms_pk<ldpc::Wifi1296_23, (true|false), (true|false)>",
     r"k_vn_ms<8, (true|false), \d>",
     r"k_cn_ms<8, (true|false), \d>",

@@ -13,10 +13,71 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from ldpc_amd.codes import wifi_code  # noqa: E402
 
 CODES = [("Wifi648_12", 648, "1/2"), ("Wifi1296_23", 1296, "2/3"), ("Wifi1944_56", 1944, "5/6")]
+ASCENT_FRAMES = {"Wifi1296_23"}  # codes that keep the round-1 frame search (lane_frames_ascent)
 
 
-def lane_frames(base, Z, trials=400, seed=1):
+def lane_frames(base, Z, trials=8000, seed=11):
     """Lane relabelling that maximises zero-shift circulants.
+
+    The kernel may hold variable (j, (z + phi_j) mod Z) in lane z and check (r, (z + psi_r) mod Z) in lane
+    z: a pure relabelling (bit-exact), under which circulant (r, j, s) becomes a rotation by
+    (s - phi_j + psi_r) mod Z, and rotation 0 needs no lane exchange (two ds_bpermute fewer per iteration).
+    Coordinate ascent over (phi, psi) from random spanning-tree starts (a spanning tree of the base graph
+    already gives MB + NB - 1 zeros), with random moves along plateaus of equal count (without them the
+    ascent stalls early: (648,1/2) 41 -> 44 zeros, (1296,2/3) 36 -> 38).  Only phi reaches the kernel
+    (LLR load / bit store index); check labels are internal."""
+    import random
+    from collections import Counter
+    mb, nb = base.shape
+    edges = [(i, j, int(base[i, j])) for i in range(mb) for j in range(nb) if base[i, j] >= 0]
+    rows = {i: [(j, s) for (ii, j, s) in edges if ii == i] for i in range(mb)}
+    cols = {j: [(i, s) for (i, jj, s) in edges if jj == j] for j in range(nb)}
+    rng = random.Random(seed)
+    best = (sum(1 for e in edges if e[2] == 0), [0] * mb, [0] * nb)
+    for _trial in range(trials):
+        psi = [rng.randrange(Z) for _ in range(mb)]
+        phi = [rng.randrange(Z) for _ in range(nb)]
+        order = edges[:]
+        rng.shuffle(order)
+        seen_r, seen_c = {rng.randrange(mb)}, set()
+        grown = True
+        while grown:  # a random spanning tree made all-zero
+            grown = False
+            for (i, j, s) in order:
+                if i in seen_r and j not in seen_c:
+                    phi[j] = (s + psi[i]) % Z
+                    seen_c.add(j)
+                    grown = True
+                elif j in seen_c and i not in seen_r:
+                    psi[i] = (phi[j] - s) % Z
+                    seen_r.add(i)
+                    grown = True
+        for _sweep in range(40):
+            for k in rng.sample(range(mb + nb), mb + nb):
+                if k < mb:
+                    c = Counter((phi[j] - s) % Z for (j, s) in rows[k])
+                    top = max(c.values())
+                    v = rng.choice([x for x, m in c.items() if m == top])
+                    if top > c[psi[k]] or (v != psi[k] and rng.random() < 0.3):
+                        psi[k] = v
+                else:
+                    jj = k - mb
+                    c = Counter((s + psi[i]) % Z for (i, s) in cols[jj])
+                    top = max(c.values())
+                    v = rng.choice([x for x, m in c.items() if m == top])
+                    if top > c[phi[jj]] or (v != phi[jj] and rng.random() < 0.3):
+                        phi[jj] = v
+            cnt = sum(1 for (i, j, s) in edges if (s - phi[j] + psi[i]) % Z == 0)
+            if cnt > best[0]:
+                best = (cnt, list(psi), list(phi))
+    return best
+
+
+def lane_frames_ascent(base, Z, trials=400, seed=1):
+    """The round-1 search (strict ascent, alternating random and spanning-tree starts): kept for (1296,2/3),
+    whose packed 5-bit kernel measured 1.2 % faster with these frames (36 zeros) than with 38 (A/B).
+
+    Lane relabelling that maximises zero-shift circulants.
 
     The kernel may hold variable (j, (z + phi_j) mod Z) in lane z and check (r, (z + psi_r) mod Z) in lane
     z: a pure relabelling (bit-exact), under which circulant (r, j, s) becomes a rotation by
@@ -73,7 +134,7 @@ def lane_frames(base, Z, trials=400, seed=1):
 def emit(name, q):
     mb, nb = q.base.shape
     rows = [[(j, int(q.base[r, j])) for j in range(nb) if q.base[r, j] >= 0] for r in range(mb)]
-    nzero, psi, phi = lane_frames(q.base, q.Z)
+    nzero, psi, phi = (lane_frames_ascent if name in ASCENT_FRAMES else lane_frames)(q.base, q.Z)
     maxdc = max(len(r) for r in rows)
     pad = lambda xs: xs + [-1] * (maxdc - len(xs))
     # Z > 64: the lifting index is split into S slots of ZL = Z / S <= 32 lanes (one wave per slot, two

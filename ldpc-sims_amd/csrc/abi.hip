@@ -8,6 +8,8 @@
 #include <stdio.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -299,22 +301,87 @@ static int pipe_alloc(ldpc_graph* g, int64_t chunk, size_t ws_bytes) {
     return LDPC_OK;
 }
 
-// Host-side work of one chunk split over worker threads (the staging copies are memory-bound).
+// Host-side work of one chunk split over worker threads (the staging copies are memory-bound).  The workers
+// are created once per process and parked on a condition variable between jobs: spawning them per chunk
+// cost ~30 us x threads x 2 per chunk.  One job at a time (run_mtx); the caller thread takes slice 0.
+class HostPool {
+  public:
+    static HostPool& get() {
+        static HostPool p;
+        return p;
+    }
+    void run(int slices, const std::function<void(int)>& job) {
+        std::lock_guard<std::mutex> one(run_mtx_);
+        ensure(slices - 1);
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &job;
+            nslices_ = slices;
+            pending_ = slices - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        job(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    void ensure(int n) {
+        while ((int)workers_.size() < n) {
+            const int id = (int)workers_.size() + 1;  // slice index served by this worker
+            workers_.emplace_back([this, id] { loop(id); });
+        }
+    }
+    void loop(int id) {
+        int64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* job;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (id >= nslices_) continue;  // not part of this job
+                job = job_;
+            }
+            (*job)(id);
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    std::mutex run_mtx_, m_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(int)>* job_ = nullptr;
+    int64_t gen_ = 0;
+    int nslices_ = 0, pending_ = 0;
+    bool stop_ = false;
+};
+
 template <class F>
 static void parallel_rows(int64_t rows, int threads, F&& f) {
     if (threads <= 1 || rows < 2 * threads) {
         f((int64_t)0, rows);
         return;
     }
-    std::vector<std::thread> ts;
-    ts.reserve(threads - 1);
     const int64_t per = (rows + threads - 1) / threads;
-    for (int t = 1; t < threads; ++t) {
+    const std::function<void(int)> job = [&](int t) {
         const int64_t a = t * per, b = std::min(rows, a + per);
-        if (a < b) ts.emplace_back([&f, a, b] { f(a, b); });
-    }
-    f((int64_t)0, std::min(rows, per));
-    for (auto& t : ts) t.join();
+        if (a < b) f(a, b);
+    };
+    HostPool::get().run(threads, job);
 }
 
 }  // namespace ldpc

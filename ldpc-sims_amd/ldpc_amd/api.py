@@ -213,8 +213,16 @@ def get_decoder(H, device: int = 0) -> Decoder:
 
 
 def decode(H, llr, max_iters: int, *, algo="tanh", clamp=10.0, alpha=1.0, beta=0.0, early_stop=False,
-           precision="f32", out="bits", device=None, **kw):
-    """``decode(H, llr, max_iters)`` -> hard bits (uint8, (B, n)); ``out="bits+soft"`` -> (bits, p1)."""
+           precision="f32", out="bits", device=None, llr_sign="p1/p0", **kw):
+    """``decode(H, llr, max_iters)`` -> hard bits (uint8, (B, n)); ``out="bits+soft"`` -> (bits, p1).
+
+    ``llr_sign``: "p1/p0" (default) = log P(1)/P(0), the reference's convention (ofdm_functions.py:72);
+    "p0/p1" = the usual communications convention (positive = bit 0), negated once before decoding (an
+    extra elementwise pass; results are those of the negated input)."""
+    if llr_sign not in ("p1/p0", "p0/p1"):
+        raise ValueError("llr_sign must be 'p1/p0' or 'p0/p1'")
+    if llr_sign == "p0/p1":
+        llr = -llr
     on_gpu = type(llr).__module__.startswith("torch") and llr.is_cuda
     if device is None:
         device = llr.device.index if on_gpu else 0

@@ -465,3 +465,16 @@ def test_packed_quantized_ragged_batches(code, B, early):
     torch.cuda.synchronize()
     assert (bits[B:] == 7).all() and (soft[B:] == 7.0).all() and (used[B:] == 77).all()
     assert np.array_equal(bits[:B].cpu().numpy(), ref["bits"])
+
+
+def test_decode_llr_sign_convention():
+    """decode(..., llr_sign="p0/p1") takes the communications convention (positive = bit 0): the same bits
+    as the reference convention on the negated input."""
+    H, _ = get_code("wifi648_12")
+    cw, llr = _llr(H, 64, 2.0, seed=3)
+    a = ldpc_amd.decode(H, llr, 10, algo="minsum", clamp=20.0)
+    b = ldpc_amd.decode(H, -llr, 10, algo="minsum", clamp=20.0, llr_sign="p0/p1")
+    c = ldpc_amd.decode(H, torch.from_numpy(-llr).cuda(), 10, algo="minsum", clamp=20.0, llr_sign="p0/p1").cpu().numpy()
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+    with pytest.raises(ValueError):
+        ldpc_amd.decode(H, llr, 10, llr_sign="bogus")

@@ -102,9 +102,10 @@ def test_decode_bits_wifi648_equals_device_path():
     dec = ldpc_amd.get_decoder(H)
     p = dec.params(20, "tanh", 10.0)
     out2 = np.zeros_like(out)
-    _abi.check(dec.lib.ldpc_decode_bits_host(dec._h, np.ascontiguousarray(llr, np.float64).ctypes.data, rows,
-                                             ctypes.byref(p), out2.ctypes.data, 333, 4))
-    assert np.array_equal(out2, out)
+    x = np.ascontiguousarray(llr, np.float64)  # held: a temporary's buffer would be freed before the call
+    _abi.check(dec.lib.ldpc_decode_bits_host(dec._h, x.ctypes.data, rows, ctypes.byref(p), out2.ctypes.data, 333, 4))
+    bad = np.nonzero((out2 != out).any(axis=1))[0]
+    assert bad.size == 0, f"rows differing: {bad[:20].tolist()} (chunks {sorted(set((bad // 333).tolist()))[:10]})"
 
 
 def test_belief_propagation_module_matches_reference_golden():

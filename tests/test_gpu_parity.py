@@ -262,6 +262,28 @@ def test_qc_quantized_minsum_vs_oracle(code, early, beta):
     assert np.array_equal(r["soft"], (0.5 * ref["app"]).astype(np.float32))
 
 
+@pytest.mark.parametrize("code", QC_CODES)
+@pytest.mark.parametrize("qmax,app_max,qstep,beta", [(7, 31, 0.5, 2), (127, 2047, 0.125, 3), (31, 32767, 1.0, 0),
+                                                     (3, 3, 2.0, 1)])
+def test_qc_quantized_minsum_quantizer_ranges(code, qmax, app_max, qstep, beta):
+    """Quantizer widths other than 5 bit: the message / APP saturations, offsets up to beta = 3 and
+    app_max above every reachable posterior (the packed kernel's fp16 halves stay exact: |L + sum c2v| <=
+    (1 + d_v) qmax <= 1651 < 2048) — bits, APP and iteration counts bitwise vs the oracle."""
+    H, qc = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, 300, 3.0 if rate < 0.6 else 4.5, seed=5 + qmax, rate=rate)
+    qs = np.float32(qstep)
+    q = np.clip(np.rint(llr * (np.float32(1.0) / qs)), -qmax, qmax).astype(np.int32)
+    dec = ldpc_amd.get_decoder(H)
+    for early in (False, True):
+        r = dec.decode(llr, 12, algo="qminsum", qmax=qmax, app_max=app_max, qstep=float(qs), beta=float(beta),
+                       early_stop=early, soft="z", want_iters=True)
+        ref = oracle.qms(H, q, 12, qmax, app_max, beta, early_stop=early)
+        assert np.array_equal(r["iters_used"], ref["iters_used"])
+        assert np.array_equal(r["bits"], ref["bits"])
+        assert np.array_equal(r["soft"], (0.5 * ref["app"]).astype(np.float32))
+
+
 def test_degenerate_graph_empty_row_and_column():
     """An all-zero row and column of H (the reference accepts any binary H, masking.py:12)."""
     H, _ = get_code("peg64_32")

@@ -817,6 +817,13 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #ifndef QC_SP_WAVES_PER_SIMD
 #define QC_SP_WAVES_PER_SIMD 4
 #endif
+// QC_SP_SERIAL: each edge's exclusive sum / product chain starts after the previous edge's tanh / log
+// output (an empty asm ties them): at most one chain in flight, instead of the scheduler interleaving a
+// row's d chains and holding their partial products in registers.  Same operations, same order.  Fixed
+// iteration count only: (648,1/2) 6.45 -> 6.79 M cw/s (A/B); the early-stop kernel is 0.5 % slower with it.
+#ifndef QC_SP_SERIAL
+#define QC_SP_SERIAL 1
+#endif
 #ifndef QC_SP_WAVES_PER_SIMD_EARLY
 #define QC_SP_WAVES_PER_SIMD_EARLY 2  // 648 tanh-SP early stop 10.2 -> 12.1 M cw/s (A/B; 3 waves: 11.1)
 #endif
@@ -936,6 +943,8 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 const float v = Num<float>::tanh_(0.5f * (L + S));
                 P += msg[e];
                 msg[e] = v;
+                if constexpr (QC_SP_SERIAL && !EARLY)
+                    asm volatile("" : "+v"(P), "+v"(msg[e]));  // next edge's sum chain starts after this output
             });
         });
         // CV in the check frame: gather v2c, exclusive products, log, clamp, scatter c2v back
@@ -961,7 +970,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 float p = Q;
                 static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
                 Q *= g[t];
-                const float y = cn_tanh_out(p, clamp);
+                float y = cn_tanh_out(p, clamp);
+                if constexpr (QC_SP_SERIAL && !EARLY)
+                    asm volatile("" : "+v"(Q), "+v"(y));  // next edge's product chain starts after this output
                 if constexpr (s == 0) {
                     msg[e0 + t] = y;
                 } else {

@@ -28,8 +28,14 @@ constexpr int nz_max() {
 #ifndef QC_SL_WAVES_PER_SIMD
 #define QC_SL_WAVES_PER_SIMD 3
 #endif
+// Per variant (fixed iteration count / EARLY) — occupancy, exchange buffers, where L lives; A/B on the box
+// (profiles/r02/ab/): fixed 1.47 -> 1.86 M cw/s with serial chains, one buffer, L from global, 4 waves;
+// early stop 2.27 -> 2.50 M cw/s with serial chains at 2 waves (3 waves / one buffer / L in global: 2.46).
 #ifndef QC_SL_SP_WAVES_PER_SIMD
-#define QC_SL_SP_WAVES_PER_SIMD 2  // spill-free (3 waves: 83 VGPRs spilled), same speed (1.446 vs 1.448 M cw/s)
+#define QC_SL_SP_WAVES_PER_SIMD 4
+#endif
+#ifndef QC_SL_SP_WAVES_PER_SIMD_EARLY
+#define QC_SL_SP_WAVES_PER_SIMD_EARLY 2
 #endif
 
 // Early stop (EARLY): before iteration it >= 1, every lane sums its columns' c2v (ascending, the generic VN
@@ -38,27 +44,42 @@ constexpr int nz_max() {
 // gather's positions) and the unit's waves pool one ballot per (slot, codeword) in LDS.  A codeword whose
 // syndrome is zero writes its outputs from z_it right there (iters_used = it) and is skipped at the end;
 // the unit leaves the loop when both of its codewords are done.  Bitwise equal to the generic path.
-// QC_SL_SP_COMPACT: L in LDS (not VGPRs) and one exchange buffer for v2c and c2v (a third barrier per
-// row instead of a second buffer): 41 instead of 52 KB of LDS and 24 fewer VGPRs per workgroup, so three
-// units fit a CU at 3 waves/SIMD without scratch.
+// QC_SL_SP_SERIAL_CN: each edge's exclusive product (CN) / sum (VN) chain starts after the previous edge's
+// log / tanh output (an empty asm ties them), so one chain is in flight instead of a row's 20 partial
+// products held in registers: 195 -> 112 VGPRs for the same operations in the same order.
+// QC_SL_SP_COMPACT: one exchange buffer for v2c and c2v (a third barrier per row instead of a second
+// buffer).  QC_SL_SP_L: where L lives — 0 VGPRs, 1 LDS, 2 re-read from global memory (an L2 hit) at every
+// use.  Fixed-count kernel: one buffer + L in global = 26 KB of LDS per unit, 112 VGPRs: five units
+// (15 waves) per CU instead of two.
+#ifndef QC_SL_SP_SERIAL_CN
+#define QC_SL_SP_SERIAL_CN 1
+#endif
 #ifndef QC_SL_SP_COMPACT
-#define QC_SL_SP_COMPACT 0  // A/B: 1.51 vs 1.45 M cw/s at 3 waves/SIMD but 19 VGPRs spilled; 1.30 at 2 waves
+#define QC_SL_SP_COMPACT 1
+#endif
+#ifndef QC_SL_SP_COMPACT_EARLY
+#define QC_SL_SP_COMPACT_EARLY 0
+#endif
+#ifndef QC_SL_SP_L
+#define QC_SL_SP_L 2
+#endif
+#ifndef QC_SL_SP_L_EARLY
+#define QC_SL_SP_L_EARLY 0
 #endif
 
 template <class C, bool EARLY>
-__global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_SL_SP_WAVES_PER_SIMD)))
+__global__ __launch_bounds__(C::S * 64)
+__attribute__((amdgpu_waves_per_eu(EARLY ? QC_SL_SP_WAVES_PER_SIMD_EARLY : QC_SL_SP_WAVES_PER_SIMD)))
 void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
                 uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
     constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB), NT = nz_max<C>(), ROW = 2 * 2 * Z;  // floats per exchanged circulant
     static_assert(S > 1 && Z % S == 0 && ZL <= 32, "sliced kernel: Z = S * ZL, ZL <= 32");
-#if QC_SL_SP_COMPACT
-    __shared__ float Xv[NT * ROW];
-    float* const Xc = Xv;
-    __shared__ float Lsh[2 * NB * Z];  // L of both codewords: [half][j][position]
-#else
-    __shared__ float Xv[NT * ROW], Xc[NT * ROW];
-#endif
+    constexpr bool CMP = EARLY ? QC_SL_SP_COMPACT_EARLY : QC_SL_SP_COMPACT;
+    constexpr int LM = EARLY ? QC_SL_SP_L_EARLY : QC_SL_SP_L;
+    __shared__ float Xv[NT * ROW], Xc2[CMP ? 1 : NT * ROW];
+    float* const Xc = CMP ? Xv : Xc2;
+    __shared__ float Lsh[LM == 1 ? 2 * NB * Z : 1];  // L of both codewords: [half][j][position]
     const int k = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // slot of this wave
     const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
     const int64_t cw = (int64_t)blockIdx.x * 2 + h;
@@ -67,37 +88,38 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     const int zc = live ? l + ZL * k : 0;    // idle lanes alias position 0 for reads (never store)
     const int xb = h * 2 * Z + zc;           // this lane's position in an exchange row
     // L = -llr (bp.py:47) of this lane's variable in every block column
-#if QC_SL_SP_COMPACT
+    const float* const lp = llr + (valid ? cw * N : 0);
     const int lb = h * NB * Z + zc;
+    float Lr[LM == 0 ? NB : 1];
     auto Lr_at = [&](int j) __attribute__((always_inline)) {
-        int a = lb;
-        asm volatile("" : "+v"(a));  // re-read every iteration, not hoisted into registers
-        return Lsh[a + j * Z];
+        if constexpr (LM == 2) {
+            int z = zc;
+            asm volatile("" : "+v"(z));  // re-read at every use (an L2 hit), not hoisted into registers
+            int t = z + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            return valid ? -lp[j * Z + t] : 0.0f;
+        } else if constexpr (LM == 1) {
+            int a = lb;
+            asm volatile("" : "+v"(a));  // re-read every iteration, not hoisted into registers
+            return Lsh[a + j * Z];
+        } else {
+            return Lr[j];
+        }
     };
-    {
-        const int64_t base = valid ? cw * N : 0;
+    if constexpr (LM != 2) {
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             int t = zc + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
-            const float x = valid ? -llr[base + j * Z + t] : 0.0f;
-            if (live) Lsh[lb + j * Z] = x;
+            const float x = valid ? -lp[j * Z + t] : 0.0f;
+            if constexpr (LM == 1) {
+                if (live) Lsh[lb + j * Z] = x;
+            } else {
+                Lr[j] = x;
+            }
         });
+        if constexpr (LM == 1) __syncthreads();
     }
-    __syncthreads();
-#else
-    float Lr[NB];
-    auto Lr_at = [&](int j) __attribute__((always_inline)) { return Lr[j]; };
-    {
-        const int64_t base = valid ? cw * N : 0;
-        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-            constexpr int j = decltype(jj)::value;
-            int t = zc + C::PHI[j];
-            t -= (t >= Z) ? Z : 0;
-            Lr[j] = valid ? -llr[base + j * Z + t] : 0.0f;
-        });
-    }
-#endif
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
@@ -200,6 +222,9 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 const float v = Num<float>::tanh_(0.5f * (Lj + Ssum));
                 P += msg[e];
                 msg[e] = v;
+#if QC_SL_SP_SERIAL_CN
+                asm volatile("" : "+v"(P), "+v"(msg[e]));  // next edge's sum chain starts after this output
+#endif
             });
         });
         // CV per block row through the LDS exchange
@@ -233,10 +258,11 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 Q *= g[t];
                 const float y = cn_tanh_out(p, clamp);
                 g[t] = y;  // g[t] is not read again (products use u > t)
-            });
-#if QC_SL_SP_COMPACT
-            __syncthreads();  // every wave has read this row's v2c before the buffer takes its c2v
+#if QC_SL_SP_SERIAL_CN
+                asm volatile("" : "+v"(Q), "+v"(g[t]));  // next edge's product chain starts after this output
 #endif
+            });
+            if constexpr (CMP) __syncthreads();  // every wave has read this row's v2c before the buffer takes its c2v
             if (live) {
                 static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                     constexpr int t = decltype(tt)::value;
@@ -254,9 +280,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 if constexpr (s == 0) msg[e0 + t] = g[t];
                 else msg[e0 + t] = Xc[nz_index<C>(r, t) * ROW + xb + (Z - s)];
             });
-#if QC_SL_SP_COMPACT
-            __syncthreads();  // ... and its c2v before the next row's v2c lands in the buffer
-#endif
+            if constexpr (CMP) __syncthreads();  // ... and its c2v before the next row's v2c lands in the buffer
         });
     }
     if (EARLY && (h ? done1 : done0)) {

@@ -7,7 +7,7 @@ name=$1; file=$2; extra=$3
 O=ldpc-sims_amd/ldpc_amd/.libldpc_hip.so.objs
 mkdir -p build_variants/.o_$name
 per=""
-case $file in qc.hip|qc_sl.hip) per="-fno-honor-nans -mllvm --amdgpu-sched-strategy=iterative-ilp";; qc_pk.hip) per="-fno-honor-nans";; esac
+case $file in qc.hip|qc_sl.hip) per="-fno-honor-nans -mllvm --amdgpu-sched-strategy=iterative-ilp";; qc_pk.hip|qc_sl_es.hip) per="-fno-honor-nans";; esac
 [ -n "$NOSCHED" ] && per="-fno-honor-nans"   # default (max-occupancy) scheduler
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Wall -Wno-unused-function \
   $per $extra -I include -I ldpc-sims_amd/csrc -c -o build_variants/.o_$name/$file.o ldpc-sims_amd/csrc/$file

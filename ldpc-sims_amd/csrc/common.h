@@ -3,9 +3,21 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ldpc_abi.h"
 
 namespace ldpc {
+
+// compile-time loop: f(integral_constant<int, i>) for i in [B, E) — every index a constant, so arrays indexed
+// by it stay in registers however large the unrolled body gets (a #pragma unroll can give up)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 
 // Hard-decision thresholds: bit = 1 iff np.round(1 - sigmoid(z)) == 1 (ofdm_functions.py:161, bp.py:51).
 // fp32: measured bit pattern by bit pattern against torch 2.10 CPU sigmoid -> z <= -1.7881392e-07.

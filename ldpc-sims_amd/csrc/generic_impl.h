@@ -216,21 +216,25 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
     Vec<T, V> P;
 #pragma unroll
     for (int i = 0; i < V; ++i) P.x[i] = T(0);
-#pragma unroll
-    for (int t = 0; t < MAXD; ++t)
+    // slots by static_for: x[] / off[] indices are constants (with #pragma unroll the V = 2 bodies were
+    // left rolled and x[] went to scratch)
+    static_for<0, MAXD>([&](auto tt) __attribute__((always_inline)) {
+        constexpr int t = decltype(tt)::value;
         if (t < d) {
             Vec<T, V> o;
 #pragma unroll
             for (int i = 0; i < V; ++i) {
                 T S = P.x[i];
-#pragma unroll
-                for (int u = t + 1; u < MAXD; ++u)
+                static_for<t + 1, MAXD>([&](auto uu) __attribute__((always_inline)) {
+                    constexpr int u = decltype(uu)::value;
                     if (u < d) S += x[u].x[i];
+                });
                 o.x[i] = Num<T>::tanh_(T(0.5) * (Lv.x[i] + S));
                 P.x[i] += x[t].x[i];
             }
             vstore<T, V>(v2c + off[t], o);
         }
+    });
     if constexpr (ES) {  // hard decision of APP_it = the final layer's z (bp.py:36-39,51)
 #pragma unroll
         for (int i = 0; i < V; ++i) hb[(int64_t)v * ldb + cw + i] = (uint8_t)Num<T>::bit(T(0.5) * (Lv.x[i] + P.x[i]));
@@ -300,21 +304,23 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
     Vec<T, V> Q;
 #pragma unroll
     for (int i = 0; i < V; ++i) Q.x[i] = T(1);
-#pragma unroll
-    for (int e = 0; e < MAXD; ++e)
+    static_for<0, MAXD>([&](auto ee) __attribute__((always_inline)) {  // constant slot indices (see k_vn_sp)
+        constexpr int e = decltype(ee)::value;
         if (e < d) {
             Vec<T, V> o;
 #pragma unroll
             for (int i = 0; i < V; ++i) {
                 T p = Q.x[i];
-#pragma unroll
-                for (int u = e + 1; u < MAXD; ++u)
+                static_for<e + 1, MAXD>([&](auto uu) __attribute__((always_inline)) {
+                    constexpr int u = decltype(uu)::value;
                     if (u < d) p *= t[u].x[i];
+                });
                 o.x[i] = cn_tanh_out(p, clamp);  // clamp p, log((1+p)/(1-p)), clamp (common.h)
                 Q.x[i] *= t[e].x[i];
             }
             store_live<T, V, ES>(c2v + (int64_t)(a + e) * ldb + cw, o, done + cw);
         }
+    });
 }
 
 template <int MAXD, bool ES, int V>

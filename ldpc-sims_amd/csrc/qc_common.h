@@ -7,14 +7,6 @@
 
 namespace ldpc {
 
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>{});
-        static_for<B + 1, E>(f);
-    }
-}
-
 // first block row whose checks touch block column j (VN adds start there, so L_j is read there)
 template <class C>
 constexpr int first_row(int j) {

@@ -268,10 +268,12 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
 #define QC_ST_TPB 256  // threads per workgroup of the stored min-sum kernel (whole waves)
 #endif
 #ifndef QC_ST_WAVES_PER_SIMD
-#define QC_ST_WAVES_PER_SIMD 4  // 128 VGPRs; measured 30.6M cw/s vs 26.2M at 3 waves (648, 50 it)
+#define QC_ST_WAVES_PER_SIMD 3  // dispatched for Z > 32 ((1296,2/3)): spill-free at 134 VGPRs, 41.0 vs 39.9 M cw/s at 4
+                                // waves (2-5 VGPRs spilled; A/B, 20 it)
 #endif
 #ifndef QC_ST_WAVES_PER_SIMD_EARLY
-#define QC_ST_WAVES_PER_SIMD_EARLY 4  // early stop keeps APP_it and the syndrome ballots live
+#define QC_ST_WAVES_PER_SIMD_EARLY 4  // early stop keeps APP_it and the syndrome ballots live: 14-15 VGPRs spill at
+                                      // 4 waves, yet 3 waves (spill-free) measured 9 % slower on (1296,2/3)
 #endif
 
 template <class C, bool QUANT, bool EARLY, int NORM>
@@ -824,6 +826,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #ifndef QC_SP_SERIAL
 #define QC_SP_SERIAL 1
 #endif
+#ifndef QC_SP_SERIAL_ES_Z64
+#define QC_SP_SERIAL_ES_Z64 1  // serial chains in the Z > 32 early-stop kernel: spill-free (6 VGPRs spilled before), same
+#endif                         // speed ((1296,2/3) 8.42 vs 8.42 M cw/s, A/B)
 #ifndef QC_SP_WAVES_PER_SIMD_EARLY
 #define QC_SP_WAVES_PER_SIMD_EARLY 2  // 648 tanh-SP early stop 10.2 -> 12.1 M cw/s (A/B; 3 waves: 11.1)
 #endif
@@ -943,7 +948,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 const float v = Num<float>::tanh_(0.5f * (L + S));
                 P += msg[e];
                 msg[e] = v;
-                if constexpr (QC_SP_SERIAL && !EARLY)
+                if constexpr (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)))
                     asm volatile("" : "+v"(P), "+v"(msg[e]));  // next edge's sum chain starts after this output
             });
         });
@@ -971,7 +976,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
                 Q *= g[t];
                 float y = cn_tanh_out(p, clamp);
-                if constexpr (QC_SP_SERIAL && !EARLY)
+                if constexpr (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)))
                     asm volatile("" : "+v"(Q), "+v"(y));  // next edge's product chain starts after this output
                 if constexpr (s == 0) {
                     msg[e0 + t] = y;

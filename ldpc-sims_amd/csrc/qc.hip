@@ -19,6 +19,8 @@
 // gathers anyway; a codeword whose syndrome is zero is emitted with iters_used = it.
 #include "qc_common.h"
 
+#include <cstdint>
+
 namespace ldpc {
 
 #ifndef QC_DIAG_NO_L
@@ -526,6 +528,15 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_LA
 #define QC_PH_LA 1  // rotations issued this many rows / columns ahead, in place: +2.5 % (A/B 38.9 vs 38.0 M cw/s; 2: +2.0 %, 3: +1.5 %; 0: the plain phased order)
 #endif
+// QC_PH_LDSROT: lane rotations through a 256-B LDS row per wave instead of ds_bpermute — every lane stores its
+// value with ds_write_addtid_b32 (address M0 + 4 * lane: no address VGPR to move), then loads the slot of lane
+// (z + rho) with ds_read_b32 at the address the ds_bpermute would have taken.  A wave's LDS operations run in
+// order, so one row serves every rotation with no wait or barrier.  Measured on the box
+// (scripts/lds_micro.hip, profiles/r02/micro/): 4.31 LDS-pipe cycles per rotation against 6.16 for ds_bpermute
+// (which moves an address and a data VGPR in and a data VGPR out) — the resource that binds this kernel.
+#ifndef QC_PH_LDSROT
+#define QC_PH_LDSROT 1
+#endif
 #ifndef QC_PH_WAVES_PER_SIMD_EARLY
 #define QC_PH_WAVES_PER_SIMD_EARLY 3  // spill-free (145 VGPRs): 648 min-sum early stop 24.6 -> 57.9 M cw/s (A/B)
 #endif
@@ -554,22 +565,41 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     __shared__ __attribute__((aligned(16))) float Ls[QC_ST_TPB * LSTR];  // lane-major L rows (qc_common.h lpos)
     const int lrow = threadIdx.x * LSTR;
 
+    constexpr bool LDSROT = QC_PH_LDSROT && !EARLY;  // early stop keeps ds_bpermute (A/B: 62.0 vs 57.0 M cw/s)
+    __shared__ float Rw[LDSROT ? QC_ST_TPB : 1];  // one 64-lane rotation row per wave
+    const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;  // this wave's row, bytes from Rw
+    const int rb4 = base4 + wrow, rb4m = base4m + wrow;        // read addresses include the row
+    if constexpr (LDSROT) {
+        // M0 = this wave's row, set once: nothing else in this kernel reads or writes M0 (the CPU test
+        // test_kernel_resources.py::test_headline_m0_written_once checks the built code); s_nop 0: an SALU write
+        // of M0 needs one wait state before an add-TID LDS instruction reads it
+        const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&Rw[0]) + (unsigned)wrow);
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" ::"s"(m0) : "memory");
+    }
+    auto xfer = [&](int addr, float x) __attribute__((always_inline)) {
+        if constexpr (LDSROT) {
+            asm volatile("ds_write_addtid_b32 %0" ::"v"(x) : "memory");
+            return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Rw) + addr);
+        } else {
+            return bperm(addr, x);
+        }
+    };
     // rotation addresses, one register per distinct shift used often enough (the others: one v_cndmask
     // per use, as k_qc_ms_st)
     int ra[Z];
     static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
         constexpr int rho = decltype(rr)::value;
         if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES)
-            ra[rho] = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(base4, base4m) + 4 * rho;
+            ra[rho] = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho;
     });
     auto rot = [&](auto rr, float x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
         constexpr int rho = decltype(rr)::value;
         if constexpr (rho == 0) {
             return x;
         } else if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES) {
-            return bperm(ra[rho], x);
+            return xfer(ra[rho], x);
         } else {
-            return bperm(sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(base4, base4m) + 4 * rho, x);
+            return xfer(sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho, x);
         }
     };
     (void)ra;

@@ -66,3 +66,29 @@ def test_generic_kernels_use_no_scratch(resources):
     assert len(hits) > 40, sorted(hits)
     bad = {d: r for d, r in hits.items() if r.get("vgpr_spill_count", 0) or r.get("private_segment_fixed_size", 0)}
     assert not bad, bad
+
+
+def test_headline_m0_written_once():
+    """k_qc_ms_ph's LDS-row rotations (ds_write_addtid_b32 addresses M0 + 4 * lane) set M0 once, before the
+    loop, in inline asm: the compiler must not write M0 anywhere else in the kernel (nor read it for another
+    purpose), or the rotations would store to the wrong row."""
+    import subprocess
+    import kernel_resources as kr
+    name = "_ZN4ldpc10k_qc_ms_phINS_10Wifi648_12ELb0ELb0ELi0EEEvPKfliffffffiPhPfPi"
+    objdump = os.path.join(os.path.dirname(kr.READELF), "llvm-objdump")
+    for co in kr.code_objects(kr.DEFAULT_LIB):
+        if name.encode() not in co:
+            continue
+        path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "ldpc_headline.co")
+        with open(path, "wb") as f:
+            f.write(co)
+        dis = subprocess.run([objdump, "-d", path], capture_output=True, text=True, check=True).stdout
+        body = dis[dis.index("<" + name + ">:"):]
+        nxt = re.search(r"\n[0-9a-f]+ <_Z", body[1:])
+        body = body[: nxt.start() + 1] if nxt else body
+        insts = [l.split("//")[0].strip() for l in body.splitlines() if l.startswith("\t")]
+        m0 = [i for i in insts if re.search(r"\bm0\b", i)]
+        assert len(m0) == 1 and m0[0].startswith("s_mov_b32 m0,"), m0
+        assert sum("ds_write_addtid_b32" in i for i in insts) >= 88, "LDS-row rotations missing"
+        return
+    pytest.fail("headline kernel not found in the built library")

@@ -24,8 +24,19 @@
 // rotation tables are qc_tables.h's, as in the float kernels.
 #include "qc_common.h"
 
+#include <cstdint>
+
 namespace ldpc {
 
+// QC_PK_LDSROT(_EARLY): lane rotations through a per-wave LDS row instead of ds_bpermute (as qc.hip's
+// QC_PH_LDSROT).  Off: this kernel is not bound by the LDS pipe — A/B 1-3 % slower in every configuration
+// ((1296,2/3) 20 it fixed 50.5 vs 49.8, early stop 49.1 vs 48.4; (648,1/2) 103 vs 102, 101 vs 98 M cw/s).
+#ifndef QC_PK_LDSROT
+#define QC_PK_LDSROT 0
+#endif
+#ifndef QC_PK_LDSROT_EARLY
+#define QC_PK_LDSROT_EARLY 0
+#endif
 #ifndef QC_PK_WAVES_PER_SIMD
 #define QC_PK_WAVES_PER_SIMD 4
 #endif
@@ -111,21 +122,38 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     __shared__ __attribute__((aligned(16))) uint32_t Ls[QC_PK_TPB * LSTR];  // lane-major packed L rows (lpos)
     const int lrow = threadIdx.x * LSTR;
 
+    // lane rotations through a per-wave LDS row (as k_qc_ms_ph, qc.hip QC_PH_LDSROT) or ds_bpermute
+    constexpr bool LDSROT = EARLY ? QC_PK_LDSROT_EARLY : QC_PK_LDSROT;
+    __shared__ uint32_t Rw[LDSROT ? QC_PK_TPB : 1];
+    const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;
+    const int rb4 = base4 + wrow, rb4m = base4m + wrow;
+    if constexpr (LDSROT) {  // M0 = this wave's row, once (nothing else here uses M0); s_nop 0: M0 -> add-TID hazard
+        const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&Rw[0]) + (unsigned)wrow);
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" ::"s"(m0) : "memory");
+    }
+    auto xfer = [&](int addr, uint32_t x) __attribute__((always_inline)) {
+        if constexpr (LDSROT) {
+            asm volatile("ds_write_addtid_b32 %0" ::"v"(x) : "memory");
+            return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(Rw) + addr);
+        } else {
+            return pbperm(addr, x);
+        }
+    };
     constexpr int MINU = (Z <= 32) ? QC_PK_ADDR_MIN_USES : QC_PK_ADDR_MIN_USES_Z64;
     int ra[Z];
     static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
         constexpr int rho = decltype(rr)::value;
         if constexpr (rot_uses<C>(rho) >= MINU)
-            ra[rho] = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(base4, base4m) + 4 * rho;
+            ra[rho] = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho;
     });
     auto rot = [&](auto rr, uint32_t x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
         constexpr int rho = decltype(rr)::value;
         if constexpr (rho == 0) {
             return x;
         } else if constexpr (rot_uses<C>(rho) >= MINU) {
-            return pbperm(ra[rho], x);
+            return xfer(ra[rho], x);
         } else {
-            return pbperm(sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(base4, base4m) + 4 * rho, x);
+            return xfer(sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho, x);
         }
     };
     (void)ra;

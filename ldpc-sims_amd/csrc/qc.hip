@@ -537,6 +537,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_LDSROT
 #define QC_PH_LDSROT 1
 #endif
+#ifndef QC_PH_LDSROT_EARLY
+#define QC_PH_LDSROT_EARLY 0  // early stop keeps ds_bpermute (A/B: 61.8 vs 61.5 M cw/s; not LDS-bound)
+#endif
 #ifndef QC_PH_WAVES_PER_SIMD_EARLY
 #define QC_PH_WAVES_PER_SIMD_EARLY 3  // spill-free (145 VGPRs): 648 min-sum early stop 24.6 -> 57.9 M cw/s (A/B)
 #endif
@@ -565,7 +568,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     __shared__ __attribute__((aligned(16))) float Ls[QC_ST_TPB * LSTR];  // lane-major L rows (qc_common.h lpos)
     const int lrow = threadIdx.x * LSTR;
 
-    constexpr bool LDSROT = QC_PH_LDSROT && !EARLY;  // early stop keeps ds_bpermute (A/B: 62.0 vs 57.0 M cw/s)
+    constexpr bool LDSROT = EARLY ? QC_PH_LDSROT_EARLY : QC_PH_LDSROT;
     __shared__ float Rw[LDSROT ? QC_ST_TPB : 1];  // one 64-lane rotation row per wave
     const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;  // this wave's row, bytes from Rw
     const int rb4 = base4 + wrow, rb4m = base4m + wrow;        // read addresses include the row

@@ -297,6 +297,22 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
     const int zb = (z < Z) ? z : z - Z;
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
+    // lane rotations through a per-wave LDS row instead of ds_bpermute (see QC_PH_LDSROT)
+    constexpr bool LDSROT = EARLY ? QC_ST_LDSROT_EARLY : QC_ST_LDSROT;
+    __shared__ float Rw[LDSROT ? 256 : 1];
+    const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;
+    if constexpr (LDSROT) {
+        const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&Rw[0]) + (unsigned)wrow);
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" ::"s"(m0) : "memory");
+    }
+    auto xfer = [&](int addr, float x) __attribute__((always_inline)) {
+        if constexpr (LDSROT) {
+            asm volatile("ds_write_addtid_b32 %0" ::"v"(x) : "memory");
+            return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Rw) + wrow + addr);
+        } else {
+            return bperm(addr, x);
+        }
+    };
     const int64_t cwbase = valid ? cw * N : 0;
     const float vmask = valid ? 1.0f : 0.0f;
     auto vidx = [&](int zz, int j, int phi) {
@@ -422,7 +438,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
                     x = msg[e0 + t];
                 } else {
                     const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(base4, base4m) + 4 * s;
-                    x = bperm(addr, msg[e0 + t]);
+                    x = xfer(addr, msg[e0 + t]);
                 }
                 v[t] = x;
             });
@@ -461,7 +477,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
                     cr = c;
                 } else {
                     const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
-                    cr = bperm(addr, c);
+                    cr = xfer(addr, c);
                 }
                 msg[e0 + t] = cr;
 #if QC_DIAG_NO_L
@@ -536,6 +552,25 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 // (which moves an address and a data VGPR in and a data VGPR out) — the resource that binds this kernel.
 #ifndef QC_PH_LDSROT
 #define QC_PH_LDSROT 1
+#endif
+// LDS-row rotations in the stored min-sum / tanh-SP kernels: off — neither is LDS-pipe bound; A/B slower in
+// every configuration ((1296,2/3) min-sum 42.1 -> 38.6, early stop 52.3 -> 44.0; (648,1/2) tanh-SP 6.75 ->
+// 6.64, early stop 12.35 -> 11.83; (1296,2/3) tanh-SP 3.32 -> 3.28 M cw/s)
+#ifndef QC_ST_LDSROT
+#define QC_ST_LDSROT 0
+#endif
+#ifndef QC_ST_LDSROT_EARLY
+#define QC_ST_LDSROT_EARLY 0
+#endif
+#ifndef QC_SP_LDSROT
+#define QC_SP_LDSROT 0
+#endif
+#ifndef QC_SP_LDSROT_EARLY
+#define QC_SP_LDSROT_EARLY 0
+#endif
+#ifndef QC_PH_XSEL
+#define QC_PH_XSEL 0  // compare-free check output in the lookahead loop (plain min-sum): A/B with LDS-row
+                      // rotations 43.05 vs 43.13 M cw/s (removes the 60 hazard s_nops, same VALU count) — off
 #endif
 #ifndef QC_PH_LDSROT_EARLY
 #define QC_PH_LDSROT_EARLY 0  // early stop keeps ds_bpermute (A/B: 61.8 vs 61.5 M cw/s; not LDS-bound)
@@ -683,11 +718,21 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         const uint32_t tot = xor_all(v) & 0x80000000u;
         const float M1 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn1, alpha, beta, clamp)) ^ tot);
         const float M2 = __uint_as_float(__float_as_uint(mag_of<NORM>(mn2, alpha, beta, clamp)) ^ tot);
-        static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-            constexpr int t = decltype(tt)::value;
-            const float mg = (fabsf(v[t]) == mn1) ? M2 : M1;
-            msg[e0 + t] = __uint_as_float(__float_as_uint(mg) ^ (__float_as_uint(v[t]) & 0x80000000u));
-        });
+        if constexpr (QC_PH_XSEL && NORM == NORM_PLAIN) {  // compare-free select, as k_qc_ms_st
+            const float A1 = mag_of<NORM>(mn1, alpha, beta, clamp), A2 = mag_of<NORM>(mn2, alpha, beta, clamp);
+            const uint32_t X = __float_as_uint(M1) ^ __float_as_uint(A2);
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                const uint32_t m = __float_as_uint(__builtin_amdgcn_fmed3f(fabsf(v[t]), A1, A2));
+                msg[e0 + t] = __uint_as_float((X ^ m) ^ (__float_as_uint(v[t]) & 0x80000000u));
+            });
+        } else {
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                const float mg = (fabsf(v[t]) == mn1) ? M2 : M1;
+                msg[e0 + t] = __uint_as_float(__float_as_uint(mg) ^ (__float_as_uint(v[t]) & 0x80000000u));
+            });
+        }
     };
     auto cn_phase_la = [&]() __attribute__((always_inline)) {
         static_for<0, (QC_PH_LA < MB ? QC_PH_LA : MB)>([&](auto rr) __attribute__((always_inline)) { gather_row(rr); });
@@ -888,6 +933,22 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     const int zb = (z < Z) ? z : z - Z;
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
+    // lane rotations through a per-wave LDS row instead of ds_bpermute (see QC_PH_LDSROT)
+    constexpr bool LDSROT = EARLY ? QC_SP_LDSROT_EARLY : QC_SP_LDSROT;
+    __shared__ float Rw[LDSROT ? 256 : 1];
+    const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;
+    if constexpr (LDSROT) {
+        const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&Rw[0]) + (unsigned)wrow);
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" ::"s"(m0) : "memory");
+    }
+    auto xfer = [&](int addr, float x) __attribute__((always_inline)) {
+        if constexpr (LDSROT) {
+            asm volatile("ds_write_addtid_b32 %0" ::"v"(x) : "memory");
+            return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Rw) + wrow + addr);
+        } else {
+            return bperm(addr, x);
+        }
+    };
     __shared__ float Ls[4 * CPW * N];
     const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
     {
@@ -998,7 +1059,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                     g[t] = msg[e0 + t];
                 } else {
                     const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(base4, base4m) + 4 * s;
-                    g[t] = bperm(addr, msg[e0 + t]);
+                    g[t] = xfer(addr, msg[e0 + t]);
                 }
             });
             float Q = 1.0f;
@@ -1015,7 +1076,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                     msg[e0 + t] = y;
                 } else {
                     const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
-                    msg[e0 + t] = bperm(addr, y);
+                    msg[e0 + t] = xfer(addr, y);
                 }
             });
         });

@@ -266,6 +266,21 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
 // oracle, operation for operation.  The register kernel is instruction-fetch bound (SQC_ICACHE_BUSY ~
 // 100%): this form executes ~12 instead of ~17 instructions (~76 instead of ~124 bytes) per edge, at
 // <= 128 VGPRs (4 waves per SIMD).
+// LDS-row rotations in the stored min-sum / tanh-SP kernels: off — neither is LDS-pipe bound; A/B slower in
+// every configuration ((1296,2/3) min-sum 42.1 -> 38.6, early stop 52.3 -> 44.0; (648,1/2) tanh-SP 6.75 ->
+// 6.64, early stop 12.35 -> 11.83; (1296,2/3) tanh-SP 3.32 -> 3.28 M cw/s)
+#ifndef QC_ST_LDSROT
+#define QC_ST_LDSROT 0
+#endif
+#ifndef QC_ST_LDSROT_EARLY
+#define QC_ST_LDSROT_EARLY 0
+#endif
+#ifndef QC_SP_LDSROT
+#define QC_SP_LDSROT 0
+#endif
+#ifndef QC_SP_LDSROT_EARLY
+#define QC_SP_LDSROT_EARLY 0
+#endif
 #ifndef QC_ST_TPB
 #define QC_ST_TPB 256  // threads per workgroup of the stored min-sum kernel (whole waves)
 #endif
@@ -552,21 +567,6 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 // (which moves an address and a data VGPR in and a data VGPR out) — the resource that binds this kernel.
 #ifndef QC_PH_LDSROT
 #define QC_PH_LDSROT 1
-#endif
-// LDS-row rotations in the stored min-sum / tanh-SP kernels: off — neither is LDS-pipe bound; A/B slower in
-// every configuration ((1296,2/3) min-sum 42.1 -> 38.6, early stop 52.3 -> 44.0; (648,1/2) tanh-SP 6.75 ->
-// 6.64, early stop 12.35 -> 11.83; (1296,2/3) tanh-SP 3.32 -> 3.28 M cw/s)
-#ifndef QC_ST_LDSROT
-#define QC_ST_LDSROT 0
-#endif
-#ifndef QC_ST_LDSROT_EARLY
-#define QC_ST_LDSROT_EARLY 0
-#endif
-#ifndef QC_SP_LDSROT
-#define QC_SP_LDSROT 0
-#endif
-#ifndef QC_SP_LDSROT_EARLY
-#define QC_SP_LDSROT_EARLY 0
 #endif
 #ifndef QC_PH_XSEL
 #define QC_PH_XSEL 0  // compare-free check output in the lookahead loop (plain min-sum): A/B with LDS-row

@@ -66,6 +66,11 @@ constexpr int nz_max() {
 #ifndef QC_SL_SP_L_EARLY
 #define QC_SL_SP_L_EARLY 0
 #endif
+// QC_SL_SP_LPF (L from global memory): the VN phase loads L of column j + 1 before column j's chains.  The
+// serial-chain asm statements order memory operations, so without it every column waits out an L2 hit.
+#ifndef QC_SL_SP_LPF
+#define QC_SL_SP_LPF 0  // A/B: 1.874 vs 1.887 M cw/s, -0.8 % (profiles/r02/ab/ab_lpf.txt): the other waves hide it
+#endif
 
 template <class C, bool EARLY>
 __global__ __launch_bounds__(C::S * 64)
@@ -207,10 +212,13 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
             }
         }
         // VC + tanh in the variable frame (as k_qc_sp_st)
+        constexpr bool LPF = LM == 2 && QC_SL_SP_LPF;
+        float Lnext = LPF ? Lr_at(0) : 0.0f;
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             constexpr int dj = col_deg<C>(j);
-            const float Lj = Lr_at(j);
+            const float Lj = LPF ? Lnext : Lr_at(j);
+            if constexpr (LPF && j + 1 < NB) Lnext = Lr_at(j + 1);  // in flight during this column's chains
             float P = 0.0f;
             static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
                 constexpr int q = decltype(kk)::value;

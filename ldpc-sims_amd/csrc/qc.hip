@@ -575,6 +575,17 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_LDSROT_EARLY
 #define QC_PH_LDSROT_EARLY 0  // early stop keeps ds_bpermute (A/B: 61.8 vs 61.5 M cw/s; not LDS-bound)
 #endif
+// QC_PH_APPB (fixed iteration count, LDS-row rotations): v2c is formed in the CHECK frame.  The VN phase
+// rotates each c2v back into a temporary for the APP sum (c2v itself stays in the check frame), stores APP_j
+// into the wave's row ONCE and every edge of column j reads it at its own shift: v2c = rot_s(APP_j) - c2v,
+// the same subtraction of the same two values as APP_j - c2v followed by the gather.  The CN phase then needs
+// no rotation; per iteration 44 + 18 row stores instead of 88 on (648,1/2), the same 88 reads.
+#ifndef QC_PH_APPB
+#define QC_PH_APPB 0  // A/B -5 % (no lookahead) / -3.5 % (lookahead, spills): profiles/r02/ab/ab_appb.txt
+#endif
+#ifndef QC_PH_APPB_LA
+#define QC_PH_APPB_LA 1  // back-rotations of column p + 1 issued before column p's sum (0: in the column's own order)
+#endif
 #ifndef QC_PH_WAVES_PER_SIMD_EARLY
 #define QC_PH_WAVES_PER_SIMD_EARLY 3  // spill-free (145 VGPRs): 648 min-sum early stop 24.6 -> 57.9 M cw/s (A/B)
 #endif
@@ -799,8 +810,85 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         });
     };
 
+#if QC_PH_LA && QC_PH_APPB
+    constexpr bool APPB = !EARLY && LDSROT;
+    constexpr int DMX = [] {
+        int m = 0;
+        for (int j = 0; j < NB; ++j) m = col_deg<C>(j) > m ? col_deg<C>(j) : m;
+        return m;
+    }();
+    auto row_put = [&](float x) __attribute__((always_inline)) {
+        asm volatile("ds_write_addtid_b32 %0" ::"v"(x) : "memory");
+    };
+    auto row_get = [&](auto rr) __attribute__((always_inline)) {  // lane (z + rho) mod Z of the last row_put
+        constexpr int rho = decltype(rr)::value;
+        int addr;
+        if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES) addr = ra[rho];
+        else addr = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho;
+        return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Rw) + addr);
+    };
+    auto back_col = [&](auto pp, float* T) __attribute__((always_inline)) {  // c2v of column lcol(p), variable frame
+        constexpr int j = lcol<C>(decltype(pp)::value);
+        static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int e = col_edge<C>(j, decltype(kk)::value);
+            constexpr int r = edge_row<C>(e), t = e - edge_off<C>(r);
+            constexpr int s = C::SHR[r][t];
+            T[decltype(kk)::value] = rot(std::integral_constant<int, (s == 0) ? 0 : Z - s>{}, msg[e]);
+        });
+    };
+    auto bcast_col = [&](auto pp, float a) __attribute__((always_inline)) {  // v2c of column lcol(p), check frames
+        constexpr int j = lcol<C>(decltype(pp)::value);
+        constexpr bool any = col_deg<C>(j) > 0 && [] {
+            for (int k = 0; k < col_deg<C>(j); ++k) {
+                const int e = col_edge<C>(j, k), r = edge_row<C>(e);
+                if (C::SHR[r][e - edge_off<C>(r)] != 0) return true;
+            }
+            return false;
+        }();
+        if constexpr (any) row_put(a);
+        static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int e = col_edge<C>(j, decltype(kk)::value);
+            constexpr int r = edge_row<C>(e), t = e - edge_off<C>(r);
+            constexpr int s = C::SHR[r][t];
+            float x;
+            if constexpr (s == 0) x = a - msg[e];
+            else x = row_get(std::integral_constant<int, s>{}) - msg[e];
+            if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
+            msg[e] = x;
+        });
+    };
+    if constexpr (APPB) {  // v2c of iteration 0 into the check frames
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) { gather_row(rr); });
+    }
+#else
+    [[maybe_unused]] constexpr bool APPB = false;
+#endif
+
     int it = 0;
     for (; it + 1 < iters; ++it) {
+#if QC_PH_LA && QC_PH_APPB
+        if constexpr (APPB) {
+            static_for<0, MB>([&](auto rr) __attribute__((always_inline)) { math_row(rr); });
+            float T[2][DMX];
+            if constexpr (QC_PH_APPB_LA) back_col(std::integral_constant<int, 0>{}, T[0]);
+            static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
+                constexpr int p = decltype(pp)::value;
+                constexpr int j = lcol<C>(p);
+                if constexpr (!QC_PH_APPB_LA) back_col(pp, T[p % 2]);
+                else if constexpr (p + 1 < NB) back_col(std::integral_constant<int, p + 1>{}, T[(p + 1) % 2]);
+                if constexpr (p % 4 == 0) {
+                    int lr = lrow;
+                    asm volatile("" : "+v"(lr));
+                    Lg = *static_cast<const f4*>(__builtin_assume_aligned(&Ls[lr + p], 16));
+                }
+                float a = Lg[p % 4];
+                static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) { a = a + T[p % 2][decltype(kk)::value]; });
+                if (QUANT) a = fminf(fmaxf(a, -app_max), app_max);
+                bcast_col(pp, a);
+            });
+            continue;
+        }
+#endif
 #if QC_PH_LA
         if constexpr (!EARLY) {
             cn_phase_la();
@@ -860,7 +948,14 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     }
     // last iteration (or early exit): outputs straight from the VN phase, column by column
     const bool early_exit = EARLY && done_groups == (G0 | G1);
-    if (!early_exit && iters > 0) cn_phase();
+    if (!early_exit && iters > 0) {
+#if QC_PH_LA && QC_PH_APPB
+        if constexpr (APPB) static_for<0, MB>([&](auto rr) __attribute__((always_inline)) { math_row(rr); });
+        else cn_phase();
+#else
+        cn_phase();
+#endif
+    }
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     const int zo = tid & 31;

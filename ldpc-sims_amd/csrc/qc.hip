@@ -284,6 +284,19 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
 #ifndef QC_ST_TPB
 #define QC_ST_TPB 256  // threads per workgroup of the stored min-sum kernel (whole waves)
 #endif
+// Early stop: a workgroup's LDS stays allocated until its slowest wave exits, so with waves that leave at
+// different iterations one-wave workgroups free CU slots sooner (A/B, profiles/r02/ab/ab_tpb.txt: (648,1/2)
+// min-sum early stop 61.9 -> 65.5 M cw/s; fixed-count kernels: 256 / 128 / 64 within noise, 256 kept).
+#ifndef QC_ST_TPB_EARLY
+#define QC_ST_TPB_EARLY 64
+#endif
+#ifndef QC_SP_TPB_EARLY
+#define QC_SP_TPB_EARLY 64  // tanh-SP early stop (k_qc_sp_st): 12.35 -> 13.97 M cw/s
+#endif
+template <bool EARLY>
+constexpr int st_tpb() { return EARLY ? QC_ST_TPB_EARLY : QC_ST_TPB; }
+template <bool EARLY>
+constexpr int sp_tpb() { return EARLY ? QC_SP_TPB_EARLY : 256; }
 #ifndef QC_ST_WAVES_PER_SIMD
 #define QC_ST_WAVES_PER_SIMD 3  // dispatched for Z > 32 ((1296,2/3)): spill-free at 134 VGPRs, 41.0 vs 39.9 M cw/s at 4
                                 // waves (2-5 VGPRs spilled; A/B, 20 it)
@@ -338,11 +351,11 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #if QC_L128
     using f4 = __attribute__((ext_vector_type(4))) float;
     constexpr int LSTR = lstr<C>(), NG = (NB + 3) / 4;
-    __shared__ __attribute__((aligned(16))) float Ls[QC_ST_TPB * LSTR];  // lane-major L rows (qc_common.h lpos)
+    __shared__ __attribute__((aligned(16))) float Ls[st_tpb<EARLY>() * LSTR];  // lane-major L rows (qc_common.h lpos)
     const int lrow = threadIdx.x * LSTR;
 #define LS_AT(row, j) Ls[(row) + lpos<C>(j)]
 #else
-    __shared__ float Ls[(QC_ST_TPB / 64) * CPW * N];
+    __shared__ float Ls[(st_tpb<EARLY>() / 64) * CPW * N];
     const int lrow = ((threadIdx.x >> 6) * CPW + half) * N + z;
 #define LS_AT(row, j) Ls[(row) + (j) * Z]
 #endif
@@ -611,11 +624,11 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     const int base4m = base4 - 4 * Z;
     using f4 = __attribute__((ext_vector_type(4))) float;
     constexpr int LSTR = lstr<C>();
-    __shared__ __attribute__((aligned(16))) float Ls[QC_ST_TPB * LSTR];  // lane-major L rows (qc_common.h lpos)
+    __shared__ __attribute__((aligned(16))) float Ls[st_tpb<EARLY>() * LSTR];  // lane-major L rows (qc_common.h lpos)
     const int lrow = threadIdx.x * LSTR;
 
     constexpr bool LDSROT = EARLY ? QC_PH_LDSROT_EARLY : QC_PH_LDSROT;
-    __shared__ float Rw[LDSROT ? QC_ST_TPB : 1];  // one 64-lane rotation row per wave
+    __shared__ float Rw[LDSROT ? st_tpb<EARLY>() : 1];  // one 64-lane rotation row per wave
     const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;  // this wave's row, bytes from Rw
     const int rb4 = base4 + wrow, rb4m = base4m + wrow;        // read addresses include the row
     if constexpr (LDSROT) {
@@ -1044,7 +1057,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
             return bperm(addr, x);
         }
     };
-    __shared__ float Ls[4 * CPW * N];
+    __shared__ float Ls[(sp_tpb<EARLY>() / 64) * CPW * N];
     const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
     {
         const int64_t cwbase = valid ? cw * N : 0;
@@ -1224,13 +1237,15 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     constexpr int CPW = (C::Z <= 32) ? 2 : 1;
     const int64_t waves = (B + CPW - 1) / CPW;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
-    const unsigned blocks_st = (unsigned)((waves + QC_ST_TPB / 64 - 1) / (QC_ST_TPB / 64));
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
+    const int tpb_st = es ? st_tpb<true>() : st_tpb<false>(), tpb_sp = es ? sp_tpb<true>() : sp_tpb<false>();
+    const unsigned blocks_st = (unsigned)((waves + tpb_st / 64 - 1) / (tpb_st / 64));
+    const unsigned blocks_sp = (unsigned)((waves + tpb_sp / 64 - 1) / (tpb_sp / 64));
     const float* x = (const float*)llr;
     float* sf = (float*)soft;
     if (p.algo == LDPC_ALGO_TANH_SP) {
-        if (es) k_qc_sp_st<C, true><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
-        else k_qc_sp_st<C, false><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+        if (es) k_qc_sp_st<C, true><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+        else k_qc_sp_st<C, false><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
     } else if (p.algo == LDPC_ALGO_QMIN_SUM && QC_PACKED != 0) {
         // two codewords per lane in packed fp16 (qc_pk.hip)
         if constexpr (std::is_same_v<C, Wifi648_12>) return qc_launch_qms_pk_wifi648_12(llr, B, p, bits, soft, used, st);
@@ -1242,9 +1257,9 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #define QL(E, N)                                                                                                  \
     do {                                                                                                          \
         if constexpr (QC_PHASED != 0 && C::Z <= 32)                                                             \
-            k_qc_ms_ph<C, true, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
+            k_qc_ms_ph<C, true, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
         else if constexpr (QC_STORED != 0)                                                                        \
-            k_qc_ms_st<C, true, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
+            k_qc_ms_st<C, true, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, true, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, qm, 1.0f, b, qm, am, qi, p.flags, bits, sf, used); \
     } while (0)
@@ -1257,9 +1272,9 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #define FL(E, N)                                                                                                  \
     do {                                                                                                          \
         if constexpr (QC_PHASED != 0 && C::Z <= 32)                                                             \
-            k_qc_ms_ph<C, false, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
+            k_qc_ms_ph<C, false, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else if constexpr (QC_STORED != 0)                                                                        \
-            k_qc_ms_st<C, false, E, N><<<blocks_st, QC_ST_TPB, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
+            k_qc_ms_st<C, false, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else                                                                                                      \
             k_qc_ms<C, false, E, N><<<blocks, 256, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
     } while (0)

@@ -49,7 +49,16 @@ namespace ldpc {
 #ifndef QC_PK_ADDR_MIN_USES_Z64
 #define QC_PK_ADDR_MIN_USES_Z64 4  // Z > 32 (one lane group): 6 address registers at 4 uses (18 at 3)
 #endif
+#ifndef QC_PK_TPB
 #define QC_PK_TPB 256
+#endif
+// early stop: one-wave workgroups (a workgroup's LDS is held until its slowest wave exits); A/B
+// profiles/r02/ab/ab_tpb.txt: config [3] 49.0 -> 50.7 M cw/s (128: 50.1); fixed count: 256 / 128 / 64 equal
+#ifndef QC_PK_TPB_EARLY
+#define QC_PK_TPB_EARLY 64
+#endif
+template <bool EARLY>
+constexpr int pk_tpb() { return EARLY ? QC_PK_TPB_EARLY : QC_PK_TPB; }
 
 using h2 = _Float16 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h2 as_h2(uint32_t x) { return __builtin_bit_cast(h2, x); }
@@ -119,12 +128,12 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     const int base4m = base4 - 4 * Z;
     using f4 = __attribute__((ext_vector_type(4))) float;
     constexpr int LSTR = lstr<C>();
-    __shared__ __attribute__((aligned(16))) uint32_t Ls[QC_PK_TPB * LSTR];  // lane-major packed L rows (lpos)
+    __shared__ __attribute__((aligned(16))) uint32_t Ls[pk_tpb<EARLY>() * LSTR];  // lane-major packed L rows (lpos)
     const int lrow = threadIdx.x * LSTR;
 
     // lane rotations through a per-wave LDS row (as k_qc_ms_ph, qc.hip QC_PH_LDSROT) or ds_bpermute
     constexpr bool LDSROT = EARLY ? QC_PK_LDSROT_EARLY : QC_PK_LDSROT;
-    __shared__ uint32_t Rw[LDSROT ? QC_PK_TPB : 1];
+    __shared__ uint32_t Rw[LDSROT ? pk_tpb<EARLY>() : 1];
     const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;
     const int rb4 = base4 + wrow, rb4m = base4m + wrow;
     if constexpr (LDSROT) {  // M0 = this wave's row, once (nothing else here uses M0); s_nop 0: M0 -> add-TID hazard
@@ -353,12 +362,13 @@ static int launch_qms_pk(const void* llr, int64_t B, const ldpc_params& p, uint8
                          hipStream_t st) {
     constexpr int CPW = (C::Z <= 32) ? 2 : 1;
     const int64_t waves = (B + 2 * CPW - 1) / (2 * CPW);
-    const unsigned blocks = (unsigned)((waves + QC_PK_TPB / 64 - 1) / (QC_PK_TPB / 64));
     const float qm = (float)p.qmax, am = (float)p.app_max, b = p.beta, qi = 1.0f / p.qstep;
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
+    const int tpb = es ? pk_tpb<true>() : pk_tpb<false>();
+    const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
     const float* x = (const float*)llr;
     float* sf = (float*)soft;
-#define PK(E, BT) k_qc_qms_pk<C, E, BT><<<blocks, QC_PK_TPB, 0, st>>>(x, B, p.iters, qm, am, b, qi, p.flags, bits, sf, used)
+#define PK(E, BT) k_qc_qms_pk<C, E, BT><<<blocks, tpb, 0, st>>>(x, B, p.iters, qm, am, b, qi, p.flags, bits, sf, used)
     if (b != 0.0f) {
         if (es) PK(true, true); else PK(false, true);
     } else {

@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the decode_bits / tanh-SP side measurements")
-    ap.add_argument("--ref-cpu-json", default=os.path.join(ROOT, "profiles", "r02", "ref_cpu_wifi648.json"),
+    ap.add_argument("--ref-cpu-json", default=os.path.join(ROOT, "profiles", "ref_cpu_wifi648.json"),
                     help="the reference's own CPU decode_bits timing (scripts/time_reference_cpu.py)")
     ap.add_argument("--counters-json", default=os.path.join(ROOT, "profiles", "counters.json"),
                     help="per-launch PMC counts per configuration (scripts/gpu_profile.sh + counters_summary.py)")
@@ -157,8 +157,10 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     gpu_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
+    my_elapsed = elapsed
     elapsed = max_over_ranks(elapsed, device="cuda")
     total_cw = world * args.steps * B
+    ranks = rank_evidence(world, rank, local, my_elapsed)
     value = total_cw / elapsed
 
     # ---- roofline ---------------------------------------------------------------------------------------
@@ -174,8 +176,10 @@ def main():
         side = side_measurements(H, dec, llrs[len(ebn0) // 2], B, args)
         ref = reference_cpu(args)
         if cpu is not None and ref is not None:
-            ref["gpu_tanh_sp_over_reference"] = side["gpu_tanh_sp"]["cw_per_s"] / ref["value"]
-            ref["dropin_over_reference"] = side["dropin"]["cw_per_s"] / ref["value"]
+            if "value" in ref:
+                ref["gpu_tanh_sp_over_reference"] = side["gpu_tanh_sp"]["cw_per_s"] / ref["value"]
+                ref["dropin_over_reference"] = side["dropin"]["cw_per_s"] / ref["value"]
+                ref["headline_over_reference"] = value / ref["value"]
             cpu["reference"] = ref
 
     if rank == 0:
@@ -201,6 +205,7 @@ def main():
                 "parallelism": f"dp{world} (codeword shards, RCCL all-reduce of error counts only)",
                 "kernel_path": kpath,
             },
+            "ranks": ranks,
             "roofline": roof,
             "cpu_baseline": cpu,
             "dropin_cw_per_s": side["dropin"]["cw_per_s"] if side else None,
@@ -211,6 +216,23 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def rank_evidence(world, rank, local, elapsed):
+    """What the process group itself reports: world size and backend from torch.distributed, and every
+    rank's device (index, name, PCI bus, UUID) and timed-region seconds, gathered to rank 0 over the same
+    group (the counter all-reduce's), so a multi-GPU record shows that RCCL saw N ranks on N GPUs."""
+    import torch
+    import torch.distributed as dist
+    props = torch.cuda.get_device_properties(local)
+    me = {"rank": rank, "local_rank": local, "device": local, "name": props.name,
+          "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")),
+          "timed_s": elapsed}
+    if world > 1 and dist.is_initialized():
+        allr = [None] * dist.get_world_size()
+        dist.all_gather_object(allr, me)
+        return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()), "per_rank": allr}
+    return {"world_size": 1, "backend": None, "per_rank": [me]}
 
 
 # MI355X (MI355X_MICROARCH.md): 8 TB/s HBM3E; 256 CUs x 4 SIMD-32 at 2.4 GHz peak engine clock; a wave64 VALU
@@ -314,8 +336,10 @@ def side_measurements(H, dec, llr_dev, B, args):
 def reference_cpu(args):
     """The reference's own CPU path, timed in the build container by scripts/time_reference_cpu.py (the
     reference cannot travel to the GPU box); carried here with its provenance."""
-    if args.code != "wifi648_12" or not os.path.exists(args.ref_cpu_json):
+    if args.code != "wifi648_12":
         return None
+    if not os.path.exists(args.ref_cpu_json):  # never silently dropped (the box must carry the record)
+        return {"missing": os.path.relpath(args.ref_cpu_json, ROOT), "kind": "reference"}
     r = json.load(open(args.ref_cpu_json))
     return {"value": r["reference_cw_per_s"], "unit": "codewords/s", "cores": r["threads"], "kind": "reference",
             "sample": f"{r['codewords']} codewords, decode_bits(llrs, H, {r['iters']}, {r['batch_size']}, "
@@ -347,7 +371,7 @@ def cpu_baseline(H, args, rate):
             q = np.clip(np.rint(x / args.qstep), -15, 15).astype(np.int8)
             oracle.qms(H, q, args.iters, early_stop=args.early_stop)
         else:
-            oracle.sp_f32(H, x, args.iters, args.clamp, early_stop=args.early_stop)
+            oracle.sp_f32(H, x, args.iters, args.clamp, early_stop=args.early_stop, stable=True)
         return time.perf_counter() - t
 
     threads = oracle.num_threads()

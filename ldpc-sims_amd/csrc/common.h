@@ -103,6 +103,144 @@ __device__ __forceinline__ double cn_tanh_out(double p, double clamp) {
     return y;
 }
 
+__device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
+
+// ---- fp32 tanh sum-product in the (D, S) form (oracle/ldpc_oracle.c cn_stable_f32) ----------------
+// The same function as bp_vc.py:27 + bp.py:29 + bp_cv.py:38-50, evaluated without the reference's
+// cancellation near |p| -> 1.  The VC side hands the check a signed a = copysign(exp(-|s|), s), s = L +
+// exclusive sum (twice the reference's tanh argument: |tanh(s/2)| = (1-a)/(1+a)).  A set of edges is a pair
+// (D, S) ~ (P+ - P-, P+ + P-) with P+- = prod(1 +- a); the identity is (0, 1), one edge adds D' = D + a*S,
+// S' = S + a*D (two fma), two sets join as D = Dp*Sq + Sp*Dq, S = Sp*Sq + Dp*Dq (products, then one add —
+// symmetric, so an edge with s = +-0, a = 1, keeps D == S exactly).  The check output of an edge is
+// log(S/D) of the set of the others (= log((1+|p|)/(1-|p|))), S/D clamped to [1, RMAX] where RMAX =
+// (1+pmax)/(1-pmax) = 16777215 is the reference's fp32 p clamp (bp_cv.py:44-47) exactly, then to the
+// caller's clamp (bp.py:47); its sign the xor of the others' signs.
+constexpr float kRmaxF32 = 16777215.0f;
+
+// exp(-|x|) with the device library's split log2(e) product (as tanh_f32 above), then the sign of x
+__device__ __forceinline__ float vn_signed_a(float x) {
+    const float t = fminf(fabsf(x), 104.0f);               // exp(-104) < 2^-149: 0 (or a flushed denormal) either way
+    const float ph = t * -0x1.715476p+0f;                  // -|x| * log2(e)
+    const float n = __builtin_rintf(ph);
+    float lo = __builtin_fmaf(t, -0x1.715476p+0f, -ph);
+    lo = __builtin_fmaf(t, -0x1.4ae0bep-26f, lo);
+    const float f = (ph - n) + lo;
+    const float e = __builtin_ldexpf(__builtin_amdgcn_exp2f(f), (int)n);
+    return __builtin_copysignf(e, x);
+}
+
+struct DSet {
+    float D, S;
+};
+__device__ __forceinline__ DSet ds_identity() { return {0.0f, 1.0f}; }
+__device__ __forceinline__ DSet ds_push(DSet x, float a) {  // a = |signed a| of one more edge
+    return {__builtin_fmaf(a, x.S, x.D), __builtin_fmaf(a, x.D, x.S)};
+}
+// log(S/D) of a set, clamped, with the given sign bit (bit 31 of sgn)
+__device__ __forceinline__ float ds_out(float D, float S, uint32_t sgn, float clamp) {
+    float r = S * __builtin_amdgcn_rcpf(D);                    // D == 0: +inf -> RMAX
+    r = __builtin_amdgcn_fmed3f(r, 1.0f, kRmaxF32);
+    const float y = fminf(log_f32_normal(r), clamp);
+    return u2f(f2u(y) | (sgn & 0x80000000u));
+}
+// the output of an edge from its prefix set p and suffix set q (the join, then ds_out)
+__device__ __forceinline__ float ds_join_out(DSet p, DSet q, uint32_t sgn, float clamp) {
+    const float D = p.D * q.S + p.S * q.D;  // -ffp-contract=off: two products and one add each
+    const float S = p.S * q.S + p.D * q.D;
+    return ds_out(D, S, sgn, clamp);
+}
+
+// One check row of compile-time degree d: g[] holds the gathered signed a of its edges (check frame) and
+// receives their outputs.  Suffix sets are built right to left, then a left-to-right pass joins each
+// edge's prefix with the suffix after it (edges 0 and d-1 need no join): 2(d-1) + 2(d-1) fma + 4(d-2)
+// products/adds.  SERIAL ties each edge's output to the running prefix (an empty asm), so the scheduler
+// keeps one edge's log in flight instead of interleaving the row's.
+#ifndef DS_SPLIT_D
+#define DS_SPLIT_D 12  // rows longer than this run in blocks (register budget of the sliced Z = 81 kernel)
+#endif
+#ifndef DS_BLOCK
+#define DS_BLOCK 7  // (1944,5/6) d = 20: 3 blocks, 128 VGPRs spill-free at 4 waves/SIMD (10: 3 VGPRs spilled)
+#endif
+template <int d, bool SERIAL>
+__device__ __forceinline__ void cn_ds_row(float (&g)[d], float clamp) {
+    uint32_t sg = 0;
+    static_for<0, d>([&](auto tt) __attribute__((always_inline)) { sg ^= f2u(g[decltype(tt)::value]); });
+    if constexpr (d == 1) {
+        g[0] = ds_out(0.0f, 1.0f, 0u, clamp);  // empty product: p = 1 -> the p clamp, positive
+    } else if constexpr (d > DS_SPLIT_D) {
+        // Long rows (802.11n 1944 5/6: d = 20) in blocks of DS_BLOCK edges, so only one block's suffix sets
+        // are live: per block, the set T of the edges after it (fresh pushes from the row's end), then the
+        // block's suffixes from T and its outputs with the running prefix.  Every set is formed by the same
+        // pushes in the same order as the unblocked pass, so the outputs are bitwise the unblocked ones; the
+        // cost is the T passes.  (Each block's T pushes copies of the inputs through an empty asm: otherwise
+        // the compiler CSEs the passes and keeps every suffix set live, which is what blocking avoids.)
+        constexpr int BS = DS_BLOCK < d ? DS_BLOCK : d, NBK = (d + BS - 1) / BS;
+        DSet pre = {0.0f, 1.0f};
+        static_for<0, NBK>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int lo = decltype(kk)::value * BS, hi = (lo + BS < d) ? lo + BS : d;
+            float sD[BS + 1], sS[BS + 1];  // sD[t - lo]: set of edges t..d-1, lo < t <= hi
+            if constexpr (hi < d) {
+                float a = fabsf(g[d - 1]);
+                asm volatile("" : "+v"(a));
+                DSet T = {a, 1.0f};
+                static_for<0, d - 1 - hi>([&](auto uu) __attribute__((always_inline)) {
+                    float b = fabsf(g[d - 2 - decltype(uu)::value]);
+                    asm volatile("" : "+v"(b));
+                    T = ds_push(T, b);
+                });
+                sD[hi - lo] = T.D;
+                sS[hi - lo] = T.S;
+            }
+            static_for<0, hi - lo - 1>([&](auto uu) __attribute__((always_inline)) {
+                constexpr int t = hi - 1 - decltype(uu)::value;  // hi-1 down to lo+1
+                if constexpr (t == d - 1) {
+                    sD[t - lo] = fabsf(g[t]);
+                    sS[t - lo] = 1.0f;
+                } else {
+                    const DSet q = ds_push({sD[t + 1 - lo], sS[t + 1 - lo]}, fabsf(g[t]));
+                    sD[t - lo] = q.D;
+                    sS[t - lo] = q.S;
+                }
+            });
+            static_for<lo, hi>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                const float a = fabsf(g[t]);
+                float y;
+                if constexpr (t == 0) y = ds_out(sD[1 - lo], sS[1 - lo], sg ^ f2u(g[t]), clamp);
+                else if constexpr (t == d - 1) y = ds_out(pre.D, pre.S, sg ^ f2u(g[t]), clamp);
+                else y = ds_join_out(pre, {sD[t + 1 - lo], sS[t + 1 - lo]}, sg ^ f2u(g[t]), clamp);
+                if constexpr (t == 0) pre = {a, 1.0f};
+                else if constexpr (t < d - 1) pre = ds_push(pre, a);
+                g[t] = y;
+                if constexpr (SERIAL) asm volatile("" : "+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+            });
+        });
+    } else {
+        float sD[d], sS[d];  // suffix set of edges t..d-1, t >= 1
+        sD[d - 1] = fabsf(g[d - 1]);
+        sS[d - 1] = 1.0f;
+        static_for<0, d - 2>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int t = d - 2 - decltype(kk)::value;
+            const DSet q = ds_push({sD[t + 1], sS[t + 1]}, fabsf(g[t]));
+            sD[t] = q.D;
+            sS[t] = q.S;
+        });
+        DSet pre = {fabsf(g[0]), 1.0f};
+        g[0] = ds_out(sD[1], sS[1], sg ^ f2u(g[0]), clamp);
+        if constexpr (SERIAL) asm volatile("" : "+v"(pre.D), "+v"(g[0]));
+        static_for<1, d - 1>([&](auto tt) __attribute__((always_inline)) {
+            constexpr int t = decltype(tt)::value;
+            const float a = fabsf(g[t]);
+            const float y = ds_join_out(pre, {sD[t + 1], sS[t + 1]}, sg ^ f2u(g[t]), clamp);
+            pre = ds_push(pre, a);
+            g[t] = y;
+            if constexpr (SERIAL) asm volatile("" : "+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+        });
+        g[d - 1] = ds_out(pre.D, pre.S, sg ^ f2u(g[d - 1]), clamp);
+    }
+}
+
 template <typename T> struct Num;
 template <> struct Num<float> {
     __device__ static float tanh_(float x) { return tanh_f32(x); }
@@ -114,9 +252,6 @@ template <> struct Num<double> {
     __device__ static double exp_(double x) { return exp(x); }
     __device__ static bool bit(double z) { return z < kZthrF64; }
 };
-
-__device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
-__device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
 
 // min-sum check-node output magnitude (oracle/ldpc_oracle.c ms_f32_one): min(clamp, max(alpha*m - beta, 0))
 __device__ __forceinline__ float ms_mag(float m, float alpha, float beta, float clamp) {

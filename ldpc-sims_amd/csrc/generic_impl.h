@@ -16,6 +16,9 @@
 //   tanh-SP  k_vn_sp : v2c = tanh(0.5*(L + sum_{c'!=c} c2v))           bp_vc.py:16-27 + bp.py:29
 //            k_cn_sp : c2v = clamp(log((1+p)/(1-p)), +-clamp), p = clamp(prod_{v'!=v} v2c, +-(1-1e-7))
 //                                                                        bp_cv.py:22-50 + bp.py:47
+//            fp32 evaluates this function in the (D, S) form (common.h): the VN stores the signed
+//            a = copysign(exp(-|s|), s) instead of tanh(s/2), the CN forms each edge's exclusive set from
+//            prefix and suffix sets (O(d)) and outputs log(S/D); fp64 keeps the reference's operations.
 //   min-sum  k_vn_ms / k_cn_ms                                          (oracle/ldpc_oracle.c spec)
 //   k_final  : z = 0.5*(L + sum c2v), bits = np.round(1-sigmoid(z)), p1 = 1-sigmoid(z)   bp.py:51
 //
@@ -229,7 +232,8 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
                     constexpr int u = decltype(uu)::value;
                     if (u < d) S += x[u].x[i];
                 });
-                o.x[i] = Num<T>::tanh_(T(0.5) * (Lv.x[i] + S));
+                if constexpr (std::is_same_v<T, float>) o.x[i] = vn_signed_a(Lv.x[i] + S);
+                else o.x[i] = Num<T>::tanh_(T(0.5) * (Lv.x[i] + S));
                 P.x[i] += x[t].x[i];
             }
             vstore<T, V>(v2c + off[t], o);
@@ -281,7 +285,8 @@ __global__ __launch_bounds__(256) void k_vn_spw(const int32_t* __restrict__ var_
 #pragma unroll
                 for (int u = 0; u < MAXD; ++u)
                     if (u < d && u != t) S += (wv ? wv[t * d + u] : T(1)) * x[u].x[i];
-                o.x[i] = Num<T>::tanh_(T(0.5) * (lw * Lv.x[i] + S));
+                if constexpr (std::is_same_v<T, float>) o.x[i] = vn_signed_a(lw * Lv.x[i] + S);
+                else o.x[i] = Num<T>::tanh_(T(0.5) * (lw * Lv.x[i] + S));
             }
             vstore<T, V>(v2c + off[t], o);
         }
@@ -301,6 +306,40 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
     Vec<T, V> t[MAXD];
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) t[k] = vload<T, V>(v2c + (int64_t)(a + (k < d ? k : d - 1)) * ldb + cw);
+    if constexpr (std::is_same_v<T, float>) {
+        // (D, S) form: slots >= d carry a = 0, whose set is the identity, so every slot runs the same code
+        DSet suf[MAXD + 1][V];
+        uint32_t sg[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            suf[MAXD][i] = ds_identity();
+            sg[i] = 0;
+        }
+        static_for<0, MAXD>([&](auto kk) __attribute__((always_inline)) {
+            constexpr int u = MAXD - 1 - decltype(kk)::value;
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                suf[u][i] = ds_push(suf[u + 1][i], u < d ? fabsf(t[u].x[i]) : 0.0f);
+                sg[i] ^= u < d ? f2u(t[u].x[i]) : 0u;
+            }
+        });
+        DSet pre[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) pre[i] = ds_identity();
+        static_for<0, MAXD>([&](auto ee) __attribute__((always_inline)) {
+            constexpr int e = decltype(ee)::value;
+            if (e < d) {
+                Vec<T, V> o;
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    o.x[i] = ds_join_out(pre[i], suf[e + 1][i], sg[i] ^ f2u(t[e].x[i]), clamp);
+                    pre[i] = ds_push(pre[i], fabsf(t[e].x[i]));
+                }
+                store_live<T, V, ES>(c2v + (int64_t)(a + e) * ldb + cw, o, done + cw);
+            }
+        });
+        return;
+    }
     Vec<T, V> Q;
 #pragma unroll
     for (int i = 0; i < V; ++i) Q.x[i] = T(1);

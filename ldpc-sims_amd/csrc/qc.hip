@@ -997,11 +997,11 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 
 // ---- tanh sum-product, register-resident (the reference's algorithm on-chip) ---------------------
 // Messages in the variable frame, one VGPR per edge (c2v between iterations, v2c inside one).  The
-// operation order is the oracle's and the generic kernels' (bp_vc.py:16-27, bp_cv.py:22-50): per
-// variable, v2c_t = tanh(0.5 * (L + S_t)) with S_t the ascending sum skipping t, formed prefix-then-
-// continue; per check, p_t = the ascending product skipping t, clamped to +-(1-1e-7), then
-// log((1+p)/(1-p)) clamped to +-clamp; final z = 0.5 * (L + ascending sum).  Same tanhf/logf/expf, so the
-// values equal the generic GPU path's.
+// operations are the oracle's (D, S) form and the generic kernels' (bp_vc.py:16-27, bp_cv.py:22-50 evaluated
+// as in common.h): per variable, v2c_t = copysign(exp(-|L + S_t|), .) with S_t the ascending sum skipping
+// t, formed prefix-then-continue; per check (cn_ds_row), each edge's log(S/D) of the others' set, clamped
+// to the reference's p clamp and to +-clamp; final z = 0.5 * (L + ascending sum).  Same device routines, so
+// the values equal the generic GPU path's.
 #ifndef QC_SP_WAVES_PER_SIMD
 #define QC_SP_WAVES_PER_SIMD 4
 #endif
@@ -1147,7 +1147,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 static_for<k + 1, dj>([&](auto uu) __attribute__((always_inline)) {
                     S += msg[col_edge<C>(j, decltype(uu)::value)];
                 });
-                const float v = Num<float>::tanh_(0.5f * (L + S));
+                const float v = vn_signed_a(L + S);  // the (D, S) form's VC output (common.h)
                 P += msg[e];
                 msg[e] = v;
                 if constexpr (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)))
@@ -1170,21 +1170,15 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                     g[t] = xfer(addr, msg[e0 + t]);
                 }
             });
-            float Q = 1.0f;
+            cn_ds_row<d, (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)))>(g, clamp);
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int s = C::SHR[r][t];
-                float p = Q;
-                static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
-                Q *= g[t];
-                float y = cn_tanh_out(p, clamp);
-                if constexpr (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)))
-                    asm volatile("" : "+v"(Q), "+v"(y));  // next edge's product chain starts after this output
                 if constexpr (s == 0) {
-                    msg[e0 + t] = y;
+                    msg[e0 + t] = g[t];
                 } else {
                     const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
-                    msg[e0 + t] = xfer(addr, y);
+                    msg[e0 + t] = xfer(addr, g[t]);
                 }
             });
         });

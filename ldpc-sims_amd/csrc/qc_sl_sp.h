@@ -227,7 +227,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 static_for<q + 1, dj>([&](auto uu) __attribute__((always_inline)) {
                     Ssum += msg[col_edge<C>(j, decltype(uu)::value)];
                 });
-                const float v = Num<float>::tanh_(0.5f * (Lj + Ssum));
+                const float v = vn_signed_a(Lj + Ssum);  // the (D, S) form's VC output (common.h)
                 P += msg[e];
                 msg[e] = v;
 #if QC_SL_SP_SERIAL_CN
@@ -258,18 +258,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 if constexpr (s == 0) g[t] = msg[e0 + t];
                 else g[t] = Xv[nz_index<C>(r, t) * ROW + xb + s];
             });
-            float Q = 1.0f;
-            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
-                constexpr int t = decltype(tt)::value;
-                float p = Q;
-                static_for<t + 1, d>([&](auto uu) __attribute__((always_inline)) { p *= g[decltype(uu)::value]; });
-                Q *= g[t];
-                const float y = cn_tanh_out(p, clamp);
-                g[t] = y;  // g[t] is not read again (products use u > t)
-#if QC_SL_SP_SERIAL_CN
-                asm volatile("" : "+v"(Q), "+v"(g[t]));  // next edge's product chain starts after this output
-#endif
-            });
+            cn_ds_row<d, QC_SL_SP_SERIAL_CN != 0>(g, clamp);  // O(d) exclusive sets (common.h)
             if constexpr (CMP) __syncthreads();  // every wave has read this row's v2c before the buffer takes its c2v
             if (live) {
                 static_for<0, d>([&](auto tt) __attribute__((always_inline)) {

@@ -45,6 +45,9 @@
 #define PMAX_F32 ((float)(1.0 - 1e-7))                /* torch casts the python bound to fp32 */
 #define PMAX_F64 (1.0 - 1e-7)
 
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
 typedef struct {
     int m, n, E;
     const int32_t *row_ptr, *col_idx, *var_ptr, *var_edges;
@@ -66,11 +69,59 @@ typedef struct {
 /* tanh sum-product, fp32 (bp/bp.py:43-51, bp_vc.py:16-27, bp_cv.py:22-50)                      */
 static int syndrome_ok(const graph_t* g, const uint8_t* bits);
 
+/* The check-node rule evaluated in the (D, S) form ("stable" mode: what the GPU kernels compute).
+ *
+ * Mathematically the same function as bp_cv.py:38-50: with s the full-LLR v2c argument (v2c = tanh(s/2),
+ * bp_vc.py:27 + bp.py:29) write a = exp(-|s|), so |tanh(s/2)| = (1-a)/(1+a).  For a set of edges let
+ * P+ = prod(1+a), P- = prod(1-a); D = P+ - P-, S = P+ + P- (up to a common positive factor).  Then
+ * |p| = |prod tanh| = (S-D)/(S+D) and log((1+|p|)/(1-|p|)) = log(S/D).  Adding one edge (a, 1):
+ * D' = D + a*S, S' = S + a*D; joining two sets: D = Dp*Sq + Sp*Dq, S = Sp*Sq + Dp*Dq — sums of positive
+ * terms only, so every step is accurate to an ulp, where the reference's fp32 form loses digits near |p| -> 1
+ * (1-p cancels; one ulp of tanh near 1 is a 1e-4..1e-3 error in log).  Exclusive (D, S) per edge from prefix
+ * and suffix sets, O(d) per check.  The clamp |p| <= 1-1e-7 is S/D <= RMAX = (1+pmax)/(1-pmax) (fp32:
+ * 16777215 = the reference's fp32 bound exactly), then the caller's clamp; sign = xor of the others' signs.
+ * An s of +-0 gives a = 1, whose set has D == S exactly (the symmetric join keeps it so): log 1 = 0 for the
+ * other edges, as the reference's p = 0. */
+#define RMAX_F32 16777215.0f  /* (1 + PMAX_F32) / (1 - PMAX_F32) in fp32 */
+static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float clamp, float* out,
+                          float* sufD, float* sufS) {
+    if (d == 1) {  /* empty product = 1 -> the p clamp */
+        const float y = logf(RMAX_F32);
+        out[0] = y > clamp ? clamp : y;
+        return;
+    }
+    uint32_t sg = 0;
+    for (int t = 0; t < d; ++t) sg ^= f2u(sa[t]);
+    sufD[d - 1] = fabsf(sa[d - 1]);
+    sufS[d - 1] = 1.0f;
+    for (int t = d - 2; t >= 1; --t) {
+        const float a = fabsf(sa[t]);
+        sufD[t] = fmaf(a, sufS[t + 1], sufD[t + 1]);
+        sufS[t] = fmaf(a, sufD[t + 1], sufS[t + 1]);
+    }
+    float pD = 0.0f, pS = 1.0f;
+    for (int t = 0; t < d; ++t) {
+        float D, S;
+        if (t == 0) { D = sufD[1]; S = sufS[1]; }
+        else if (t == d - 1) { D = pD; S = pS; }
+        else { D = pD * sufS[t + 1] + pS * sufD[t + 1]; S = pS * sufS[t + 1] + pD * sufD[t + 1]; }
+        float r = S / D;                      /* D == 0 (every other a underflowed): +inf -> RMAX */
+        if (!(r <= RMAX_F32)) r = RMAX_F32;
+        float y = logf(r);
+        if (y > clamp) y = clamp;
+        out[t] = u2f(f2u(y) | ((sg ^ f2u(sa[t])) & 0x80000000u));
+        const float a = fabsf(sa[t]);
+        const float nD = fmaf(a, pS, pD), nS = fmaf(a, pD, pS);
+        pD = nD;
+        pS = nS;
+    }
+}
+
 /* early stop (not in the reference): after iteration it >= 1, stop when the final layer's decisions
  * z = 0.5*(L + sum x) (bp.py:36-39,51) satisfy every check; returns the iterations run. */
 static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp, float* x, float* v2c,
                       float* p1_out, float* z_out, uint8_t* bits_out, float* trace, int64_t trace_stride,
-                      int early_stop, uint8_t* hb, const wts_t* w) {
+                      int early_stop, uint8_t* hb, const wts_t* w, int stable, float* sufD, float* sufS) {
     const int E = g->E;
     int used = iters;
     for (int e = 0; e < E; ++e) x[e] = 0.0f;
@@ -93,11 +144,20 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
                 float S = 0.0f;
                 for (int u = a; u < b; ++u)
                     if (u != t) S += wv ? wv[(t - a) * d + (u - a)] * x[g->var_edges[u]] : x[g->var_edges[u]];
-                v2c[g->var_edges[t]] = tanhf(0.5f * (Lw + S));
+                if (stable) {  /* signed a = copysign(exp(-|s|), s), s = 2 * the reference's tanh argument */
+                    const float sv = Lw + S;
+                    v2c[g->var_edges[t]] = copysignf(expf(-fabsf(sv)), sv);
+                } else {
+                    v2c[g->var_edges[t]] = tanhf(0.5f * (Lw + S));
+                }
             }
         }
         /* CV */
-        for (int c = 0; c < g->m; ++c) {
+        for (int c = 0; c < g->m && stable; ++c) {
+            const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
+            cn_stable_f32(b - a, v2c + a, clamp, x + a, sufD, sufS);
+        }
+        for (int c = 0; c < g->m && !stable; ++c) {
             const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
             for (int e = a; e < b; ++e) {
                 float p = 1.0f;
@@ -170,9 +230,6 @@ static void sp_f64_one(const graph_t* g, const double* llr, int iters, double cl
         if (bits_out) bits_out[v] = (uint8_t)(z < ZTHR_F64);
     }
 }
-
-static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
-static inline float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
 
 static int syndrome_ok(const graph_t* g, const uint8_t* bits) {
     for (int c = 0; c < g->m; ++c) {
@@ -312,9 +369,11 @@ static const wts_t* make_wts(const graph_t* g, wts_t* wt, WEIGHT_ARGS) {
     return wt;
 }
 
+/* stable = 0: the reference's fp32 operations (tanh, masked product, log((1+p)/(1-p))); 1: the (D, S) form
+ * of cn_stable_f32, the specification the GPU tanh-SP kernels follow. */
 int oracle_sp_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clamp, float* p1, float* z,
                   uint8_t* bits, float* trace /* [iters][B][E] or NULL */, int early_stop, int32_t* iters_used,
-                  WEIGHT_ARGS) {
+                  WEIGHT_ARGS, int stable) {
     MAKE_GRAPH;
     wts_t wt;
     const wts_t* w = make_wts(&g, &wt, w_vn, w_lw, w_fin, w_flw);
@@ -323,13 +382,16 @@ int oracle_sp_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clam
     {
         float* x = (float*)malloc(sizeof(float) * (size_t)E);
         float* v2c = (float*)malloc(sizeof(float) * (size_t)E);
+        float* suf = (float*)malloc(sizeof(float) * 2 * (size_t)E);
         uint8_t* hb = (uint8_t*)malloc((size_t)n);
 #pragma omp for schedule(dynamic, 16)
         for (int64_t i = 0; i < B; ++i) {
             int u = sp_f32_one(&g, llr + i * n, iters, clamp, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
-                               bits ? bits + i * n : NULL, trace ? trace + i * E : NULL, B * (int64_t)E, early_stop, hb, w);
+                               bits ? bits + i * n : NULL, trace ? trace + i * E : NULL, B * (int64_t)E, early_stop, hb, w,
+                               stable, suf, suf + E);
             if (iters_used) iters_used[i] = u;
         }
+        free(suf);
         free(x);
         free(v2c);
         free(hb);

@@ -37,7 +37,7 @@ def lib():
         vp = ctypes.c_void_p
         garg = [ctypes.c_int, ctypes.c_int, ctypes.c_int, i32p, i32p, i32p, i32p]
         L.oracle_sp_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, vp, vp, vp, vp,
-                                           ctypes.c_int, vp] + [vp] * 4
+                                           ctypes.c_int, vp] + [vp] * 4 + [ctypes.c_int]
         L.oracle_sp_f64.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, vp, vp, vp] + [vp] * 4
         L.oracle_ms_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                            ctypes.c_float, ctypes.c_int, vp, vp, vp, vp]
@@ -72,8 +72,11 @@ def _weights(weights, dtype):
     return [_ptr(a) for a in arrs], arrs
 
 
-def sp_f32(H, llr, iters, clamp, trace=False, early_stop=False, weights=None):
-    """tanh sum-product in fp32. Returns dict(p1, z, bits, iters_used[, trace[iters,B,E]])."""
+def sp_f32(H, llr, iters, clamp, trace=False, early_stop=False, weights=None, stable=False):
+    """tanh sum-product in fp32. Returns dict(p1, z, bits, iters_used[, trace[iters,B,E]]).
+
+    stable=False: the reference's own fp32 operations (bp_vc.py:27, bp_cv.py:38-50); stable=True: the same
+    function in the (D, S) form the GPU kernels compute (ldpc_oracle.c cn_stable_f32)."""
     g = _graph(H)
     wp, _keep = _weights(weights, np.float32)
     llr = np.ascontiguousarray(llr, dtype=np.float32)
@@ -84,7 +87,7 @@ def sp_f32(H, llr, iters, clamp, trace=False, early_stop=False, weights=None):
     tr = np.empty((iters, B, g.E), np.float32) if trace else None
     used = np.empty(B, np.int32)
     lib().oracle_sp_f32(*_gargs(g), _ptr(llr), B, int(iters), float(clamp), _ptr(p1), _ptr(z), _ptr(bits), _ptr(tr),
-                        int(bool(early_stop)), _ptr(used), *wp)
+                        int(bool(early_stop)), _ptr(used), *wp, int(bool(stable)))
     out = dict(p1=p1, z=z, bits=bits, iters_used=used)
     if trace:
         out["trace"] = tr

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-2 GPU session: full GPU tests (soft-parity / overlay log), smoke, the bench line, per-config lines.
+# GPU session: full GPU tests (soft-parity / overlay log), smoke, the bench line, per-config lines.
+#   OUT=gpurun_out/<name> bash scripts/gpu_session.sh
 set -o pipefail
-OUT=${OUT:-gpurun_out/r2b}
+OUT=${OUT:-gpurun_out/session}
 mkdir -p $OUT
 export TMPDIR=/tmp
 rm -f $OUT/soft_parity.jsonl

@@ -2,7 +2,7 @@
 """Time the REFERENCE's own CPU decode path on the real 802.11n (648,1/2) H (build container only).
 
 The reference (/root/reference/pytorch) never travels to the GPU box, so its CPU throughput is measured
-here, once, and committed as profiles/r02/ref_cpu_wifi648.json; bench.py carries it in
+here, once, and committed as profiles/ref_cpu_wifi648.json; bench.py carries it in
 ``cpu_baseline.reference`` with this provenance.  What is timed is exactly what every reference evaluator
 calls: ``decode_bits(llrs, H, 50, batch_size, clamp)`` (``pytorch/ofdm/ofdm_functions.py:131-163``), i.e.
 ``BeliefPropagation(H, 50)`` (tanh sum-product, ``bp/bp.py:20-51``) batch by batch, with torch's
@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--clamp", type=float, default=10.0)
     ap.add_argument("--ebn0", type=float, default=2.5)
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02", "ref_cpu_wifi648.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "ref_cpu_wifi648.json"))
     a = ap.parse_args()
 
     sys.path.insert(0, REF)

@@ -1,17 +1,19 @@
 """Soft-output parity against the reference's float64 output (north_star: soft outputs within 1e-5).
 
-The reference's own fp32 forward is not a fixed target: near |p| -> 1 its fp32 `log((1+p)/(1-p))`
-(`bp/bp_cv.py:44-50`) is ill-conditioned, so torch-fp32 and any other fp32 evaluation (ours: the same
-operations with the GPU's tanhf/logf/expf) drift apart from each other and from fp64 on a few entries.
-The rule used by every soft-parity test:
+The decoder's fp32 tanh-SP evaluates the reference's check rule (`bp/bp_cv.py:38-50`) in the (D, S) form
+(`ldpc-sims_amd/csrc/common.h`, `oracle/ldpc_oracle.c` cn_stable_f32): sums of positive terms instead of the
+reference's `log((1+p)/(1-p))`, whose `1-p` cancels near |p| -> 1 (one fp32 ulp of tanh there is a 1e-4..1e-3
+error in the log).  So the target is the reference's fp64 output, and the rules are:
 
-* **p1** (`BeliefPropagation.forward`'s output, `bp/bp.py:51`): on every entry where the reference's
-  fp32 p1 is within 1e-5 of the reference's fp64 p1 ("well-conditioned"), ours must be within 1e-5 of
-  the reference's fp64 p1.  The excluded (ill-conditioned) entries are counted and reported.
-* **z** (the final VC output, `bp_vc.py:16-27` with `mask_v_final`; an LLR of magnitude up to ~50,
-  where one fp32 ulp is 4e-6): ours must stay inside the reference's own fp32 error envelope,
-  |z - z64| <= Z_ENVELOPE * max(|z32 - z64|, 1e-5 * max(1, |z64|)), i.e. no worse than a small factor of
-  what the reference itself achieves in fp32, and 1e-5-relative where the reference's fp32 is.
+* **p1** (`BeliefPropagation.forward`'s output, `bp/bp.py:51`; absolute) and
+* **z** (the final VC output, `bp_vc.py:16-27` with `mask_v_final`; an LLR up to ~50; relative to max(1, |z|)):
+  - on every codeword the reference DECODES (its fp64 hard decision satisfies every check — H b = 0):
+    |z - z64| <= 1e-5 * max(1, |z64|) on **every** entry, no exclusions;
+  - on decoding failures (oscillating / non-convergent codewords) BP's iteration map amplifies any fp32
+    rounding (fp64 VN sums change nothing there: DESIGN.md §4), so fp32 cannot follow fp64 to 1e-5 after
+    tens of iterations — the reference's own fp32 is off by up to 2e-3 there.  Ours must stay within 1e-5
+    or within the reference's own fp32 error on the failing codewords of the same set, whichever is larger;
+    the entries where the reference's fp32 meets 1e-5 and ours does not are counted and logged.
 
 Each check appends its measured maxima to $LDPC_PARITY_LOG (JSON lines) when that is set; the GPU
 scripts collect them into profiles/.
@@ -22,7 +24,6 @@ import os
 import numpy as np
 
 TOL = 1e-5
-Z_ENVELOPE = 3.0  # measured maximum ratio 2.70 (GPU and C oracle alike; profiles/r02/soft_parity.jsonl)
 
 
 def _log(rec):
@@ -33,38 +34,61 @@ def _log(rec):
             f.write(json.dumps(rec) + "\n")
 
 
-def check_p1(label, got, ref32, ref64, tol=TOL):
-    """got/ref32/ref64: p1 arrays of one shape.  Returns the record (also logged)."""
+def check_p1(label, got, ref32, ref64, H, tol=TOL):
+    """got/ref32/ref64: p1 arrays of one shape; H the code.  On codewords the reference decodes (its fp64
+    decision p1 > 0.5 satisfies H) every entry within `tol` of the fp64 p1; on decoding failures within
+    max(tol, the reference's own fp32 error there).  Returns the record (also logged)."""
     got = np.asarray(got, np.float64)
     ref32 = np.asarray(ref32, np.float64)
     ref64 = np.asarray(ref64, np.float64)
-    ok = np.abs(ref32 - ref64) <= tol
     err = np.abs(got - ref64)
-    rec = {"label": label, "kind": "p1", "entries": int(err.size), "excluded_ill_conditioned": int((~ok).sum()),
-           "max_abs_vs_ref_f64_on_well_conditioned": float(err[ok].max()) if ok.any() else 0.0,
-           "max_abs_vs_ref_f64_all": float(err.max()) if err.size else 0.0,
-           "ref_f32_vs_ref_f64_max": float(np.abs(ref32 - ref64).max()) if err.size else 0.0,
+    ref_err = np.abs(ref32 - ref64)
+    conv = decoded_rows(H, 0.5 - ref64)  # p1 > 0.5 <=> bit 1 <=> z < 0
+    fail_env = float(ref_err[~conv].max()) if (~conv).any() else 0.0
+    rec = {"label": label, "kind": "p1", "entries": int(err.size), "decoded_codewords": int(conv.sum()),
+           "codewords": int(err.shape[0]),
+           "max_abs_on_decoded": float(err[conv].max()) if conv.any() else 0.0,
+           "ref_f32_max_abs_on_decoded": float(ref_err[conv].max()) if conv.any() else 0.0,
+           "max_abs_on_failures": float(err[~conv].max()) if (~conv).any() else 0.0,
+           "ref_f32_max_abs_on_failures": fail_env,
+           "failures_entries_gt_tol_where_ref_f32_within": int(((err > tol) & (ref_err <= tol) & ~conv[:, None]).sum()),
            "tol": tol}
     _log(rec)
-    bad = int((err[ok] > tol).sum())
-    assert bad == 0, f"{label}: {bad} well-conditioned p1 entries off by > {tol}: {rec}"
+    bad = int((err[conv] > tol).sum())
+    assert bad == 0, f"{label}: {bad} p1 entries of decoded codewords off by > {tol}: {rec}"
+    assert rec["max_abs_on_failures"] <= max(tol, fail_env), f"{label}: p1 on decoding failures outside max({tol}, " \
+                                                             f"the reference's own fp32 error there): {rec}"
     return rec
 
 
-def check_z(label, got, z32, z64, envelope=Z_ENVELOPE):
+def decoded_rows(H, z64):
+    """Codewords whose fp64 reference hard decision (z < 0 <=> bit 1) satisfies every check of H."""
+    b = (np.asarray(z64) < 0).astype(np.int64)
+    return ~((b @ np.asarray(H, np.int64).T) % 2).any(axis=1)
+
+
+def check_z(label, got, z32, z64, H):
     got = np.asarray(got, np.float64)
     z32 = np.asarray(z32, np.float64)
     z64 = np.asarray(z64, np.float64)
     scale = np.maximum(1.0, np.abs(z64))
-    ref_err = np.abs(z32 - z64)
-    err = np.abs(got - z64)
-    ok = ref_err <= TOL * scale
-    ratio = err / np.maximum(ref_err, TOL * scale)
-    rec = {"label": label, "kind": "z", "entries": int(err.size), "ref_f32_outside_1e-5_rel": int((~ok).sum()),
-           "max_rel_vs_ref_f64_where_ref_f32_within_1e-5": float((err / scale)[ok].max()) if ok.any() else 0.0,
-           "entries_rel_gt_1e-5_where_ref_f32_within": int(((err / scale)[ok] > TOL).sum()),
-           "max_abs_vs_ref_f64": float(err.max()), "ref_f32_max_abs_vs_ref_f64": float(ref_err.max()),
-           "max_envelope_ratio": float(ratio.max()), "envelope": envelope}
+    err = np.abs(got - z64) / scale
+    ref_err = np.abs(z32 - z64) / scale
+    conv = decoded_rows(H, z64)
+    fail_env = float(ref_err[~conv].max()) if (~conv).any() else 0.0
+    tol_fail = max(TOL, fail_env)
+    ref_ok = ref_err <= TOL
+    rec = {"label": label, "kind": "z", "entries": int(err.size), "codewords": int(err.shape[0]),
+           "decoded_codewords": int(conv.sum()),
+           "max_rel_on_decoded": float(err[conv].max()) if conv.any() else 0.0,
+           "ref_f32_max_rel_on_decoded": float(ref_err[conv].max()) if conv.any() else 0.0,
+           "max_rel_on_failures": float(err[~conv].max()) if (~conv).any() else 0.0,
+           "ref_f32_max_rel_on_failures": fail_env,
+           "failures_entries_rel_gt_1e-5_where_ref_f32_within": int(((err > TOL) & ref_ok & ~conv[:, None]).sum()),
+           "tol": TOL}
     _log(rec)
-    assert rec["max_envelope_ratio"] <= envelope, f"{label}: z outside the reference's fp32 envelope: {rec}"
+    bad = int((err[conv] > TOL).sum())
+    assert bad == 0, f"{label}: {bad} z entries of decoded codewords off by > {TOL} relative: {rec}"
+    assert rec["max_rel_on_failures"] <= tol_fail, f"{label}: z on decoding failures outside max(1e-5, the " \
+                                                   f"reference's own fp32 error there): {rec}"
     return rec

@@ -4,7 +4,9 @@
 Goldens were produced by the reference itself (tests/golden/make_golden.py):
 * bp_peg64_snr*.npz: the (64,32) PEG code, Eb/N0 {0,2,4} x (iters, clamp) {(3,20),(5,10),(10,10),(10,100),(50,10)};
 * bp_<802.11n code>_sp.npz: (648,1/2) 128 codewords, (1296,2/3) and (1944,5/6) 32 codewords each, 5 iterations,
-  clamp 10, p1 and z in fp32 and fp64 (`bp/bp.py:43-51`, `bp_vc.py:16-27`, `bp_cv.py:22-50`).
+  clamp 10, p1 and z in fp32 and fp64 (`bp/bp.py:43-51`, `bp_vc.py:16-27`, `bp_cv.py:22-50`);
+* bp_<802.11n code>_sp_it<k>.npz: the same at the iteration counts the drop-in and the BASELINE configs run —
+  (648,1/2) 50 iterations x 192 codewords, (1296,2/3) 20 x 96, (1944,5/6) 10 x 48, clamp 10.
 Both kernel families run every file: the register/sliced QC kernels ("auto") and the generic CSR kernels.
 Hard decisions must equal the reference's fp32 hard decisions exactly.
 """
@@ -24,7 +26,11 @@ import ldpc_amd  # noqa: E402
 from ldpc_amd.codes import qc_expand  # noqa: E402
 
 PEG_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_peg64_snr*.npz")))
-WIFI_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_wifi*_sp.npz")))
+WIFI_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_wifi*_sp*.npz")))
+
+
+def _name(p):
+    return os.path.basename(p)[3:-4]
 
 
 @pytest.mark.parametrize("path", PEG_FILES, ids=lambda p: os.path.basename(p)[:-4])
@@ -34,10 +40,10 @@ def test_peg64_p1_vs_reference_f64(path):
     r = dec.decode(torch.from_numpy(d["llr"]).cuda(), int(d["iters"]), algo="tanh", clamp=float(d["clamp"]), soft="p1")
     p1 = r["soft"].cpu().numpy()
     assert np.array_equal(r["bits"].cpu().numpy(), d["bits_f32"])
-    check_p1(os.path.basename(path)[:-4], p1, d["p1_f32"], d["p1_f64"])
+    check_p1(os.path.basename(path)[:-4], p1, d["p1_f32"], d["p1_f64"], d["H"])
 
 
-@pytest.mark.parametrize("path", WIFI_FILES, ids=lambda p: os.path.basename(p)[3:-7])
+@pytest.mark.parametrize("path", WIFI_FILES, ids=_name)
 @pytest.mark.parametrize("path_kind", ["auto", "generic"])
 def test_wifi_p1_and_z_vs_reference_f64(path, path_kind):
     d = np.load(path)
@@ -46,7 +52,7 @@ def test_wifi_p1_and_z_vs_reference_f64(path, path_kind):
     if path_kind == "auto":
         assert dec.qc_z == int(d["Z"])  # the QC kernel family is the one under test
     iters, clamp = int(d["iters"]), float(d["clamp"])
-    name = os.path.basename(path)[3:-7]
+    name = _name(path)
     for snr in d["snrs"]:
         tag = f"snr{snr:g}".replace(".", "p")
         x = torch.from_numpy(d[f"llr_{tag}"]).cuda()
@@ -57,11 +63,11 @@ def test_wifi_p1_and_z_vs_reference_f64(path, path_kind):
         assert np.array_equal(rp["bits"].cpu().numpy(), ref_bits)
         assert np.array_equal(rz["bits"].cpu().numpy(), ref_bits)
         label = f"{name} {tag} {path_kind}"
-        check_p1(label, rp["soft"].cpu().numpy(), d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"])
-        check_z(label, rz["soft"].cpu().numpy(), d[f"z_f32_{tag}"], d[f"z_f64_{tag}"])
+        check_p1(label, rp["soft"].cpu().numpy(), d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"], H)
+        check_z(label, rz["soft"].cpu().numpy(), d[f"z_f32_{tag}"], d[f"z_f64_{tag}"], H)
 
 
-@pytest.mark.parametrize("path", WIFI_FILES, ids=lambda p: os.path.basename(p)[3:-7])
+@pytest.mark.parametrize("path", WIFI_FILES, ids=_name)
 def test_wifi_f64_vs_reference_f64(path):
     """precision='f64' (generic kernels) against the reference's .double() module."""
     d = np.load(path)
@@ -71,5 +77,6 @@ def test_wifi_f64_vs_reference_f64(path):
         tag = f"snr{snr:g}".replace(".", "p")
         llr = d[f"llr_{tag}"].astype(np.float64)
         r = dec.decode(llr, int(d["iters"]), algo="tanh", clamp=float(d["clamp"]), soft="z", precision="f64")
-        assert np.abs(r["soft"] - d[f"z_f64_{tag}"]).max() <= 1e-10 * max(1.0, np.abs(d[f"z_f64_{tag}"]).max())
+        tol = 1e-10 if int(d["iters"]) <= 10 else 1e-8  # fp64 rounding, amplified on decoding failures at 50 it
+        assert np.abs(r["soft"] - d[f"z_f64_{tag}"]).max() <= tol * max(1.0, np.abs(d[f"z_f64_{tag}"]).max())
         assert np.array_equal(r["bits"], np.round(d[f"p1_f64_{tag}"]).astype(np.uint8))

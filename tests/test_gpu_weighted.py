@@ -37,7 +37,7 @@ def test_module_weighted_matches_reference(tag):
     x = torch.zeros(llr.shape[0], m.layer_size(), device="cuda")
     p1 = m(x, llr, CLAMP).cpu().numpy()
     ref = D[f"p1_f32_{tag}"]
-    check_p1(f"weighted peg64 {tag}", p1, ref, D[f"p1_f64_{tag}"])
+    check_p1(f"weighted peg64 {tag}", p1, ref, D[f"p1_f64_{tag}"], D["H"])
     assert np.array_equal(np.round(p1), np.round(ref))
     p64 = m.double()(x.double(), llr.double(), CLAMP).cpu().numpy()
     assert np.abs(p64 - D[f"p1_f64_{tag}"]).max() < 1e-10
@@ -59,7 +59,7 @@ def test_weighted_vs_oracle(code):
     llr = (rng.standard_normal((300, g.n)) * 2.5 + 1.5).astype(np.float32)
     d = get_decoder(H)
     r = d.decode(torch.from_numpy(llr).cuda(), iters, algo="tanh", clamp=10.0, soft="z", weights=w)
-    o = oracle.sp_f32(g, llr, iters, 10.0, weights={k: v.astype(np.float32) for k, v in w.items()})
+    o = oracle.sp_f32(g, llr, iters, 10.0, weights={k: v.astype(np.float32) for k, v in w.items()}, stable=True)
     z = r["soft"].cpu().numpy()
     rel = float((np.abs(z.astype(np.float64) - o["z"]) / np.maximum(1.0, np.abs(o["z"]))).max())
     _log({"label": f"weighted_vs_oracle {code}", "kind": "z_rel_vs_oracle", "max": rel})

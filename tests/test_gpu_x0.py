@@ -35,7 +35,7 @@ def test_forward_with_initial_messages(gold, name, iters, where):
     assert p1.device.type == where
     p1 = p1.cpu().numpy()
     r32, r64 = gold[f"{name}_it{iters}_p1_f32"], gold[f"{name}_it{iters}_p1_f64"]
-    check_p1(f"x0 {name} it{iters} {where}", p1, r32, r64)
+    check_p1(f"x0 {name} it{iters} {where}", p1, r32, r64, H)
     assert np.array_equal(np.round(p1), np.round(r32))
     if where == "cuda":
         p64 = m.double()(x.double(), llr.double(), 10.0).cpu().numpy()

@@ -122,28 +122,61 @@ def test_adc_golden_self_consistent():
         assert np.isclose(d[f"clip_agc{i}"], np.std(rx) * r, rtol=1e-15)
 
 
-WIFI_SP_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_wifi*_sp.npz")))
+WIFI_SP_FILES = sorted(glob.glob(os.path.join(GOLDEN, "bp_wifi*_sp*.npz")))
 
 
-@pytest.mark.parametrize("path", WIFI_SP_FILES, ids=lambda p: os.path.basename(p)[3:-7])
+@pytest.mark.parametrize("path", WIFI_SP_FILES, ids=lambda p: os.path.basename(p)[3:-4])
 def test_oracle_wifi_codes_match_reference(path):
-    """(648,1/2), (1296,2/3), (1944,5/6) through the reference module itself (make_golden.py gen_wifi_sp):
-    the oracle's fp64 p1/z follow the reference's .double() to rounding, its fp32 hard bits equal the
-    reference's fp32 hard bits, and its fp32 soft outputs satisfy the soft-parity rule
+    """(648,1/2), (1296,2/3), (1944,5/6) through the reference module itself (make_golden.py gen_wifi_sp at 5
+    iterations, gen_wifi_sp_long at 50 / 20 / 10): the oracle's fp64 p1/z follow the reference's .double() to
+    rounding; its fp32 restatement of the reference's operations gives the reference's fp32 hard bits; its
+    (D, S) form — the GPU kernels' specification — gives the same bits and satisfies the soft-parity rule
     (tests/softparity.py) that the GPU tests apply."""
     from ldpc_amd.codes import qc_expand
     from softparity import check_p1, check_z
     d = np.load(path)
     H = qc_expand(d["base"], int(d["Z"]))
     iters, clamp = int(d["iters"]), float(d["clamp"])
-    assert len(WIFI_SP_FILES) == 3
+    assert len(WIFI_SP_FILES) == 6
     for snr in d["snrs"]:
         tag = f"snr{snr:g}".replace(".", "p")
         llr = d[f"llr_{tag}"]
         r64 = oracle.sp_f64(H, llr.astype(np.float64), iters, clamp)
-        assert np.abs(r64["p1"] - d[f"p1_f64_{tag}"]).max() <= TOL_P1_F64
-        assert np.abs(r64["z"] - d[f"z_f64_{tag}"]).max() <= 1e-11
+        # fp64 vs fp64 in another summation order: rounding, amplified ~1e3x by 50 iterations on decoding failures
+        t64 = TOL_P1_F64 if iters <= 10 else 1e-9
+        assert np.abs(r64["p1"] - d[f"p1_f64_{tag}"]).max() <= t64
+        assert np.abs(r64["z"] - d[f"z_f64_{tag}"]).max() <= 10 * t64 * max(1.0, np.abs(d[f"z_f64_{tag}"]).max())
+        ref_bits = np.round(d[f"p1_f32_{tag}"]).astype(np.uint8)
         r32 = oracle.sp_f32(H, llr, iters, clamp)
-        assert np.array_equal(r32["bits"], np.round(d[f"p1_f32_{tag}"]).astype(np.uint8))
-        check_p1(f"oracle {path}", r32["p1"], d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"])
-        check_z(f"oracle {path}", r32["z"], d[f"z_f32_{tag}"], d[f"z_f64_{tag}"])
+        assert np.array_equal(r32["bits"], ref_bits)
+        rs = oracle.sp_f32(H, llr, iters, clamp, stable=True)
+        assert np.array_equal(rs["bits"], ref_bits)
+        label = f"oracle-ds {os.path.basename(path)[3:-4]} {tag}"
+        check_p1(label, rs["p1"], d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"], H)
+        check_z(label, rs["z"], d[f"z_f32_{tag}"], d[f"z_f64_{tag}"], H)
+
+
+def test_looped_reference_golden_settings():
+    """The long-iteration goldens are the drop-in's / BASELINE configs' settings."""
+    want = {"wifi648_12": (50, 192), "wifi1296_23": (20, 96), "wifi1944_56": (10, 48)}
+    for name, (iters, cws) in want.items():
+        d = np.load(os.path.join(GOLDEN, f"bp_{name}_sp_it{iters}.npz"))
+        assert int(d["iters"]) == iters and float(d["clamp"]) == 10.0
+        assert sum(d[f"llr_snr{s:g}".replace(".", "p")].shape[0] for s in d["snrs"]) == cws
+
+
+def test_ds_form_identities():
+    """The (D, S) check rule on hand cases: d = 2 passes the other edge's LLR through, an s = 0 edge zeroes the
+    others' messages exactly (the reference's p = 0), a lone edge gets the p-clamp ceiling, the clamp binds."""
+    H = np.array([[1, 1, 1, 0], [0, 1, 1, 1]])
+    llr = np.array([[2.0, -3.0, 0.0, 1.5], [4.0, 40.0, 1.0, -2.5]], np.float32)
+    r = oracle.sp_f32(H, llr, 1, 100.0, trace=True, stable=True)
+    x = r["trace"][0]                       # check-order c2v after one iteration, edges (0,0) (0,1) (0,2) (1,1) (1,2) (1,3)
+    assert x[0, 0] == 0.0 and x[0, 1] == 0.0  # codeword 0: variable 2 has s = 0 -> edges of check 0 other than it are 0
+    f = oracle.sp_f32(H, llr, 1, 100.0, trace=True)["trace"][0]
+    assert np.allclose(x, f, rtol=2e-5, atol=1e-6)
+    H1 = np.array([[1]])
+    r1 = oracle.sp_f32(H1, np.array([[0.5]], np.float32), 1, 100.0, trace=True, stable=True)
+    assert r1["trace"][0, 0, 0] == np.float32(np.log(np.float32(16777215.0)))
+    r2 = oracle.sp_f32(H1, np.array([[0.5]], np.float32), 1, 10.0, trace=True, stable=True)
+    assert r2["trace"][0, 0, 0] == np.float32(10.0)

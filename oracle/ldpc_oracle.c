@@ -85,6 +85,7 @@ static int syndrome_ok(const graph_t* g, const uint8_t* bits);
 #define RMAX_F32 16777215.0f  /* (1 + PMAX_F32) / (1 - PMAX_F32) in fp32 */
 static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float clamp, float* out,
                           float* sufD, float* sufS) {
+    if (d == 0) return;  /* an empty check (all-zero row of H) has no edges */
     if (d == 1) {  /* empty product = 1 -> the p clamp */
         const float y = logf(RMAX_F32);
         out[0] = y > clamp ? clamp : y;

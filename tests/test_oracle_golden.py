@@ -180,3 +180,16 @@ def test_ds_form_identities():
     assert r1["trace"][0, 0, 0] == np.float32(np.log(np.float32(16777215.0)))
     r2 = oracle.sp_f32(H1, np.array([[0.5]], np.float32), 1, 10.0, trace=True, stable=True)
     assert r2["trace"][0, 0, 0] == np.float32(10.0)
+
+
+def test_degenerate_graph_both_forms():
+    """An all-zero row and column of H (the reference accepts any binary H, masking.py:12): both fp32 forms
+    decode it (no out-of-range edge access for the empty check) with the same hard bits."""
+    H = np.array(np.load(os.path.join(GOLDEN, "peg64_32.npz"))["H"])
+    H = np.concatenate([H, np.zeros((1, 64), H.dtype)], axis=0)
+    H = np.concatenate([H, np.zeros((33, 1), H.dtype)], axis=1)
+    llr = np.random.default_rng(4).normal(2.0, 2.0, size=(100, 65)).astype(np.float32)
+    a = oracle.sp_f32(H, llr, 7, 20.0)
+    b = oracle.sp_f32(H, llr, 7, 20.0, stable=True)
+    assert np.array_equal(a["bits"], b["bits"])
+    assert np.allclose(a["z"], b["z"], rtol=1e-4, atol=1e-4)

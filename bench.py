@@ -201,6 +201,7 @@ def main():
                             f"B={B} codewords/GPU/step, Eb/N0 {args.ebn0} dB cycled per step",
                 "code": args.code, "n": n, "k": k, "edges": E, "algo": args.algo, "iters": args.iters,
                 "clamp": args.clamp, "alpha": args.alpha, "early_stop": args.early_stop, "mod": args.mod,
+                "ebn0": args.ebn0, "seed": args.seed,
                 "batch_per_gpu": B, "global_batch": B * world,
                 "parallelism": f"dp{world} (codeword shards, RCCL all-reduce of error counts only)",
                 "kernel_path": kpath,
@@ -251,7 +252,8 @@ def roofline(n, E, B, launch_ms, args, kpath):
     * The register-resident QC kernels keep all messages on chip (HBM sees only llr in / bits out), so
       HBM cannot bind them: bound = the busier of VALU issue and the LDS pipe (ds_bpermute lane
       rotations), from the per-launch instruction / LDS-cycle counts that scripts/gpu_profile.sh measured
-      for this exact configuration (profiles/counters.json; deterministic for a fixed iteration count)
+      for this exact configuration (profiles/counters.json; deterministic for a fixed iteration count; for
+      early stop they depend on the data, so the record must also have this Eb/N0 grid and seed)
       divided by this run's event-timed launch duration, against 2.4 GHz peak.  The survey's byte model
       is kept beside it as hbm.model_frac (it exceeds 1 for on-chip kernels by construction) with the
       measured PMC traffic.
@@ -261,12 +263,17 @@ def roofline(n, E, B, launch_ms, args, kpath):
     launch_s = launch_ms * 1e-3
     model_gbps = bpc * B / launch_s / 1e9
     rec = None
+    note = None
     if os.path.exists(args.counters_json):
         want = {"code": args.code, "algo": args.algo, "iters": args.iters, "early_stop": args.early_stop,
                 "batch_per_gpu": B, "kernel_path": kpath, "mod": args.mod}
+        if args.early_stop:  # the work done depends on the data (iterations to convergence): same grid and seed
+            want.update(ebn0=args.ebn0, seed=args.seed)
         for r in json.load(open(args.counters_json)):
             if all(r["config"].get(k) == v for k, v in want.items()):
                 rec = r
+        if rec is None and args.early_stop:
+            note = "no counter record for this Eb/N0 grid and seed (early-stop work depends on the data)"
     c = rec["counters_per_launch"] if rec else {}
     hbm_bytes = rec["derived"].get("hbm_bytes") if rec else None
     hbm = {"model_bytes_per_codeword": bpc, "model_GBps": model_gbps, "model_frac": model_gbps / HBM_PEAK_GBPS,
@@ -274,7 +281,7 @@ def roofline(n, E, B, launch_ms, args, kpath):
            "traffic_GBps": hbm_bytes / launch_s / 1e9 if hbm_bytes else None,
            "traffic_frac": hbm_bytes / launch_s / 1e9 / HBM_PEAK_GBPS if hbm_bytes else None}
     out = {"launch_ms": launch_ms, "hbm": hbm,
-           "counters": (os.path.relpath(args.counters_json, ROOT) + f" [{rec['name']}]") if rec else None}
+           "counters": (os.path.relpath(args.counters_json, ROOT) + f" [{rec['name']}]") if rec else note}
     if kpath == "generic-csr" or "SQ_INSTS_VALU" not in c:
         out.update(bound="hbm", achieved=model_gbps, peak=HBM_PEAK_GBPS, unit="GB/s",
                    frac=model_gbps / HBM_PEAK_GBPS, traffic=hbm_bytes)

@@ -110,8 +110,9 @@ class Decoder:
                want_bits=True, want_iters=False, weights=None, x0=None):
         """Decode a (B, n) batch of LLRs (log P1/P0).  numpy in -> numpy out (host staging inside the
         library); torch GPU tensor in (on this decoder's device) -> torch GPU tensors out, asynchronous on
-        ``stream`` (a ``torch.cuda.Stream``; default: the current stream; a side stream first waits for the
-        current one, and the outputs are allocated on and ordered by the side stream) with a
+        ``stream`` (a ``torch.cuda.Stream`` or a raw ``hipStream_t`` handle as an int; default: the current
+        stream; a side stream first waits for the current one, every input it reads is kept allocated until
+        it has read it, and the outputs are allocated on and ordered by the side stream) with a
         torch-allocated workspace.  Returns dict(bits, soft, iters_used).
         ``weights``: weighted BP (tanh-SP only), compact layout of ``Graph.compact_weights``.
         ``x0``: initial c2v messages (B, E) in check-order — the reference's ``x`` (``bp/bp.py:43-47``);
@@ -144,11 +145,18 @@ class Decoder:
                 raise ValueError(f"llr is on {llr.device}, this decoder's graph is on cuda:{self.device}")
             cur = torch.cuda.current_stream(llr.device)
             ext = cur if stream is None else stream
+            if isinstance(ext, int) and not isinstance(ext, bool):  # a raw hipStream_t handle
+                ext = torch.cuda.ExternalStream(ext, device=llr.device)
             if not isinstance(ext, torch.cuda.Stream):
-                raise TypeError("stream must be a torch.cuda.Stream (or None: the current stream)")
-            if ext != cur:
+                raise TypeError("stream must be a torch.cuda.Stream, an int stream handle, or None (current stream)")
+            side = ext != cur
+            if side:
                 ext.wait_stream(cur)        # llr (and the caller's prior work) is ordered before the decode
-                llr.record_stream(ext)      # the caller's llr stays allocated until the decode has read it
+                # every tensor the decode reads stays allocated until the decode stream has read it: the
+                # caller's llr / x0 and the weights uploaded on the current stream
+                for t in [llr, x0] + list(_wkeep or []):
+                    if t is not None:
+                        t.record_stream(ext)
             tdt = torch.float64 if precision == "f64" else torch.float32
             # conversion, outputs and workspace all live on the decode stream: the allocator recycles them in
             # that stream's order, and results are ready once `ext` reaches this point
@@ -173,8 +181,8 @@ class Decoder:
                            sft.data_ptr() if sft is not None else None,
                            used.data_ptr() if used is not None else None, ws.data_ptr(), wsb,
                            ctypes.c_void_p(ext.cuda_stream)))
-            # ws is returned with the outputs so it stays alive until the caller drops the result
-            return dict(bits=bits, soft=sft, iters_used=used, workspace=ws)
+            # ws (and the weights) are returned with the outputs so they stay alive until the caller drops the result
+            return dict(bits=bits, soft=sft, iters_used=used, workspace=ws, weights=_wkeep)
         if is_torch:
             llr = llr.detach().cpu().numpy()
         x = np.ascontiguousarray(llr, dtype=fdt)

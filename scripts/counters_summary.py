@@ -67,7 +67,8 @@ def main():
     c = {cn: statistics.median(v) for (k, cn), v in vals.items() if k == kname}
     cfg = bench["config"]
     rec = {"name": a.name, "kernel": kname.split("(")[0],
-           "config": {k: cfg.get(k) for k in ("code", "algo", "iters", "early_stop", "batch_per_gpu", "mod", "kernel_path")},
+           "config": {k: cfg.get(k) for k in ("code", "algo", "iters", "early_stop", "batch_per_gpu", "mod", "kernel_path",
+                                                      "ebn0", "seed")},
            "bench": {"value": bench["value"], "ms_per_step": bench["ms_per_step"],
                      "launch_ms_events": bench["roofline"]["launch_ms"]},
            "kernel_stats": ks, "counters_per_launch": c}

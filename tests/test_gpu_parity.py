@@ -442,8 +442,27 @@ def test_side_stream_and_device_checks():
         del x                              # recycled only after the side stream has read it
         side.synchronize()
         assert torch.equal(r["bits"], want["bits"]) and torch.equal(r["soft"], want["soft"])
+    r = dec.decode(src, 10, algo="minsum", clamp=20.0, soft="z", stream=side.cuda_stream)  # a raw handle
+    side.synchronize()
+    assert torch.equal(r["bits"], want["bits"]) and torch.equal(r["soft"], want["soft"])
     with pytest.raises(TypeError):
-        dec.decode(src, 10, stream=side.cuda_stream)
+        dec.decode(src, 10, stream="side")
+    # weighted and initial-message decodes on the side stream: the weights (uploaded on the current stream)
+    # and the caller's x0 are held until the side stream has read them
+    g = dec.graph
+    rng = np.random.default_rng(3)
+    w = {"vn": rng.uniform(0.5, 1.5, (6, dec.weights_per_iter)).astype(np.float32),
+         "llr": rng.uniform(0.5, 1.5, (6, g.n)).astype(np.float32)}
+    want_w = dec.decode(src, 6, algo="tanh", soft="z", weights=w)
+    want_x = dec.decode(src, 6, algo="tanh", soft="z", x0=torch.full((300, g.E), 0.25, device="cuda"))
+    for _ in range(3):
+        x0 = torch.full((300, g.E), 0.25, device="cuda")
+        rw = dec.decode(src, 6, algo="tanh", soft="z", weights=w, stream=side)
+        rx = dec.decode(src, 6, algo="tanh", soft="z", x0=x0, stream=side)
+        del x0
+        torch.empty((300, g.E), device="cuda").fill_(7.0)   # would reuse x0's block if it were released early
+        side.synchronize()
+        assert torch.equal(rw["soft"], want_w["soft"]) and torch.equal(rx["soft"], want_x["soft"])
     with pytest.raises(ValueError):
         ldpc_amd.decode(H, src, 5, device=src.device.index + 1)
 

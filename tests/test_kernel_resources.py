@@ -68,27 +68,35 @@ def test_generic_kernels_use_no_scratch(resources):
     assert not bad, bad
 
 
-def test_headline_m0_written_once():
-    """k_qc_ms_ph's LDS-row rotations (ds_write_addtid_b32 addresses M0 + 4 * lane) set M0 once, before the
-    loop, in inline asm: the compiler must not write M0 anywhere else in the kernel (nor read it for another
-    purpose), or the rotations would store to the wrong row."""
+def _kernel_bodies():
+    """{mangled kernel symbol: [instructions]} over every gfx950 code object of the built library."""
     import subprocess
     import kernel_resources as kr
-    name = "_ZN4ldpc10k_qc_ms_phINS_10Wifi648_12ELb0ELb0ELi0EEEvPKfliffffffiPhPfPi"
     objdump = os.path.join(os.path.dirname(kr.READELF), "llvm-objdump")
-    for co in kr.code_objects(kr.DEFAULT_LIB):
-        if name.encode() not in co:
-            continue
-        path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "ldpc_headline.co")
+    out = {}
+    for k, co in enumerate(kr.code_objects(kr.DEFAULT_LIB)):
+        path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"ldpc_co_{os.getpid()}_{k}.co")
         with open(path, "wb") as f:
             f.write(co)
         dis = subprocess.run([objdump, "-d", path], capture_output=True, text=True, check=True).stdout
-        body = dis[dis.index("<" + name + ">:"):]
-        nxt = re.search(r"\n[0-9a-f]+ <_Z", body[1:])
-        body = body[: nxt.start() + 1] if nxt else body
-        insts = [l.split("//")[0].strip() for l in body.splitlines() if l.startswith("\t")]
+        os.unlink(path)
+        for m in re.finditer(r"\n[0-9a-f]+ <(_Z[^>]+)>:\n(.*?)(?=\n[0-9a-f]+ <_Z|\Z)", dis, re.S):
+            out[m.group(1)] = [l.split("//")[0].strip() for l in m.group(2).splitlines() if l.startswith("\t")]
+    return out
+
+
+def test_lds_row_rotation_kernels_write_m0_once():
+    """Every kernel that rotates lanes through an LDS row (ds_write_addtid_b32 stores to M0 + 4 * lane: the
+    headline k_qc_ms_ph in every non-early-stop instantiation — plain, alpha / beta / both normalised, float-
+    register quantized — and any other variant built with its LDS-row option) sets M0 once, in inline asm
+    before the loop: the compiler must not write M0 anywhere else in it (nor read it for another purpose), or
+    the rotations would store to the wrong row."""
+    bodies = _kernel_bodies()
+    rot = {k: v for k, v in bodies.items() if any("ds_write_addtid_b32" in i for i in v)}
+    ph = [k for k in bodies if k.startswith("_ZN4ldpc10k_qc_ms_ph") and "ELb0ELb0E" in k]  # QUANT=0, EARLY=0
+    assert len(ph) == 4 and set(ph) <= set(rot), (sorted(ph), sorted(rot))      # NORM 0..3 all rotate via LDS rows
+    for k, insts in rot.items():
         m0 = [i for i in insts if re.search(r"\bm0\b", i)]
-        assert len(m0) == 1 and m0[0].startswith("s_mov_b32 m0,"), m0
-        assert sum("ds_write_addtid_b32" in i for i in insts) >= 88, "LDS-row rotations missing"
-        return
-    pytest.fail("headline kernel not found in the built library")
+        assert len(m0) == 1 and m0[0].startswith("s_mov_b32 m0,"), (k, m0)
+    head = "_ZN4ldpc10k_qc_ms_phINS_10Wifi648_12ELb0ELb0ELi0EEEvPKfliffffffiPhPfPi"
+    assert sum("ds_write_addtid_b32" in i for i in rot[head]) >= 88, "LDS-row rotations missing"

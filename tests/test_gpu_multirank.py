@@ -62,6 +62,9 @@ def test_bench_two_ranks_equal_one_process_over_both_shards():
     two = _bench_line(_launch([*common, "--gpus", "2", "--batch", "4096"], 2))
     one = _bench_line(_launch([*common, "--gpus", "1", "--batch", "8192"], 1))
     assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 8192 and two["value"] > 0
+    rk = two["ranks"]   # what the process group itself reports, gathered over it
+    assert rk["world_size"] == 2 and rk["backend"] == "gloo" and [r["rank"] for r in rk["per_rank"]] == [0, 1]
+    assert one["ranks"]["world_size"] == 1
     assert two["ber"]["codewords_per_point"] == one["ber"]["codewords_per_point"] == 8192
     assert two["ber"]["coded_ber_info"] == one["ber"]["coded_ber_info"]
     assert two["ber"]["coded_bler"] == one["ber"]["coded_bler"]
@@ -78,3 +81,20 @@ def test_sweep_two_ranks_equal_one_process(tmp_path):
     assert two["codewords"] == one["codewords"] == [10000] * 3
     for key in ("uncoded_ber", "coded_ber", "coded_bler"):
         assert two[key] == one[key], key
+
+
+def test_bench_dvbs2_config4_two_ranks_equal_one_process():
+    """BASELINE config [4]'s sharded leg on its own code: DVB-S2 (EN 302 307) 64800 rate 1/2, 50 min-sum
+    iterations, the batch sharded over 2 ranks (256 codewords each) with the counter all-reduce — summed
+    counts equal one process decoding both shards (the reference's multi-GPU mode it replaces:
+    nn.DataParallel, ofdm_functions.py:141-145)."""
+    common = ["bench.py", "--code", "dvbs2_12", "--iters", "50", "--steps", "1", "--warmup", "0",
+              "--ebn0", "1.2:0.2:1.6", "--no-cpu-baseline", "--no-dropin"]
+    two = _bench_line(_launch([*common, "--gpus", "2", "--batch", "256"], 2, timeout=400))
+    one = _bench_line(_launch([*common, "--gpus", "1", "--batch", "512"], 1, timeout=400))
+    assert two["ranks"]["world_size"] == 2 and two["config"]["global_batch"] == 512
+    assert two["config"]["kernel_path"] == "generic-csr" and two["config"]["iters"] == 50
+    assert two["ber"]["codewords_per_point"] == one["ber"]["codewords_per_point"] == 512
+    assert two["ber"]["coded_ber_info"] == one["ber"]["coded_ber_info"]
+    assert two["ber"]["coded_bler"] == one["ber"]["coded_bler"]
+    assert one["ber"]["coded_bler"][0] > 0 and one["ber"]["coded_bler"][-1] < one["ber"]["coded_bler"][0]

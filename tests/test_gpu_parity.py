@@ -297,24 +297,39 @@ def test_degenerate_graph_empty_row_and_column():
         assert np.array_equal(r["bits"], ref["bits"])
 
 
-@pytest.mark.parametrize("name", ["dvbs2_12", "dvbs2s_12"])
-def test_dvbs2_minsum_bit_exact_and_sp_bits(name):
-    """BASELINE config [4]'s code (EN 302 307 rate 1/2, codes.dvbs2_12) and the shaped stand-in: min-sum bits
-    and z bitwise vs the oracle, tanh-SP bits identical; the reference cannot instantiate n = 64800
-    (dense E x E masks, masking.py:36-38), so parity against the reference is unpinned here."""
+@pytest.mark.parametrize("name,B,iters", [("dvbs2_12", 32, 50), ("dvbs2s_12", 6, 12)])
+def test_dvbs2_minsum_bit_exact_and_sp_bits(name, B, iters):
+    """BASELINE config [4]'s code (EN 302 307 rate 1/2, codes.dvbs2_12) at its 50 iterations on 32 codewords,
+    and the shaped stand-in: min-sum bits and z bitwise vs the oracle (plain min-sum as config [4] runs it, and
+    normalised), tanh-SP bits identical and z within the oracle tolerance; the reference cannot instantiate
+    n = 64800 (dense E x E masks, masking.py:36-38), so parity against the reference is unpinned here."""
     from ldpc_amd.codes import IRAEncoder
     c, _ = get_code(name)
     rng = np.random.default_rng(9)
-    cw = IRAEncoder(c).encode(rng.integers(0, 2, size=(6, c.k)))
-    sigma = np.sqrt(1.0 / (2 * 0.5 * 10 ** (1.0 / 10)))
+    cw = IRAEncoder(c).encode(rng.integers(0, 2, size=(B, c.k)))
+    sigma = np.sqrt(1.0 / (2 * 0.5 * 10 ** (0.9 / 10)))   # the waterfall: some codewords converge, some do not
     llr = (-2.0 * ((1.0 - 2.0 * cw) + sigma * rng.standard_normal(cw.shape)) / sigma**2).astype(np.float32)
     dec = ldpc_amd.get_decoder(c)
-    r = dec.decode(torch.from_numpy(llr).cuda(), 12, algo="minsum", alpha=0.75, clamp=20.0, soft="z")
-    ref = oracle.ms_f32(c, llr, 12, 20.0, 0.75, 0.0)
-    assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])
-    assert np.array_equal(r["soft"].cpu().numpy().view(np.uint32), ref["z"].view(np.uint32))
-    r = dec.decode(llr, 6, algo="tanh", clamp=10.0)
-    assert (r["bits"] != oracle.sp_f32(c, llr, 6, 10.0, stable=True)["bits"]).sum() == 0
+    x = torch.from_numpy(llr).cuda()
+    for alpha in (1.0, 0.75):
+        r = dec.decode(x, iters, algo="minsum", alpha=alpha, clamp=20.0, soft="z")
+        ref = oracle.ms_f32(c, llr, iters, 20.0, alpha, 0.0)
+        assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])
+        assert np.array_equal(r["soft"].cpu().numpy().view(np.uint32), ref["z"].view(np.uint32))
+    r = dec.decode(x, iters, algo="tanh", clamp=10.0, soft="z")
+    ref = oracle.sp_f32(c, llr, iters, 10.0, stable=True)
+    # codewords the oracle decodes (zero syndrome): bits identical, z to the oracle tolerance; on decoding
+    # failures 50 iterations amplify ulp-level exp/log differences (DESIGN §4), so only their count is compared
+    par = np.add.reduceat(ref["bits"][:, c.col_idx].astype(np.int64), c.row_ptr[:-1], axis=1) % 2
+    ok = ~par.any(axis=1)
+    got_bits = r["bits"].cpu().numpy()
+    assert ok.sum() >= B // 4 and np.array_equal(got_bits[ok], ref["bits"][ok])
+    gpar = np.add.reduceat(got_bits[:, c.col_idx].astype(np.int64), c.row_ptr[:-1], axis=1) % 2
+    assert abs(int((~gpar.any(axis=1)).sum()) - int(ok.sum())) <= max(1, B // 16)
+    z = r["soft"].cpu().numpy().astype(np.float64)[ok]
+    rel = np.abs(z - ref["z"][ok]) / np.maximum(1.0, np.abs(ref["z"][ok]))
+    _log({"label": f"sp_vs_oracle {name} {iters} it decoded", "kind": "z_rel_vs_oracle", "max": float(rel.max())})
+    assert rel.max() <= TOL_Z_REL_VS_ORACLE
 
 
 @pytest.mark.parametrize("code", ["peg64_32", "wifi648_12", "wifi1944_56"])

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "common.h"
+#include "host_pipeline.h"
 
 struct ldpc_graph {
     int m = 0, n = 0, E = 0, device = 0;
@@ -301,89 +302,6 @@ static int pipe_alloc(ldpc_graph* g, int64_t chunk, size_t ws_bytes) {
     return LDPC_OK;
 }
 
-// Host-side work of one chunk split over worker threads (the staging copies are memory-bound).  The workers
-// are created once per process and parked on a condition variable between jobs: spawning them per chunk
-// cost ~30 us x threads x 2 per chunk.  One job at a time (run_mtx); the caller thread takes slice 0.
-class HostPool {
-  public:
-    static HostPool& get() {
-        static HostPool p;
-        return p;
-    }
-    void run(int slices, const std::function<void(int)>& job) {
-        std::lock_guard<std::mutex> one(run_mtx_);
-        ensure(slices - 1);
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            job_ = &job;
-            nslices_ = slices;
-            pending_ = slices - 1;
-            ++gen_;
-        }
-        cv_.notify_all();
-        job(0);
-        std::unique_lock<std::mutex> lk(m_);
-        done_.wait(lk, [&] { return pending_ == 0; });
-        job_ = nullptr;
-    }
-    ~HostPool() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : workers_) t.join();
-    }
-
-  private:
-    void ensure(int n) {
-        while ((int)workers_.size() < n) {
-            const int id = (int)workers_.size() + 1;  // slice index served by this worker
-            workers_.emplace_back([this, id] { loop(id); });
-        }
-    }
-    void loop(int id) {
-        int64_t seen = 0;
-        for (;;) {
-            const std::function<void(int)>* job;
-            {
-                std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                if (id >= nslices_) continue;  // not part of this job
-                job = job_;
-            }
-            (*job)(id);
-            {
-                std::lock_guard<std::mutex> lk(m_);
-                if (--pending_ == 0) done_.notify_one();
-            }
-        }
-    }
-    std::mutex run_mtx_, m_;
-    std::condition_variable cv_, done_;
-    std::vector<std::thread> workers_;
-    const std::function<void(int)>* job_ = nullptr;
-    int64_t gen_ = 0;
-    int nslices_ = 0, pending_ = 0;
-    bool stop_ = false;
-};
-
-template <class F>
-static void parallel_rows(int64_t rows, int threads, F&& f) {
-    if (threads <= 1 || rows < 2 * threads) {
-        f((int64_t)0, rows);
-        return;
-    }
-    const int64_t per = (rows + threads - 1) / threads;
-    const std::function<void(int)> job = [&](int t) {
-        const int64_t a = t * per, b = std::min(rows, a + per);
-        if (a < b) f(a, b);
-    };
-    HostPool::get().run(threads, job);
-}
-
 }  // namespace ldpc
 
 using namespace ldpc;
@@ -619,48 +537,35 @@ int ldpc_decode_bits_host(const ldpc_graph* gc, const double* llr, int64_t rows,
     for (int i = 0; i < 2; ++i)  // a previous call that failed midway may still have copies in flight
         if ((e = hipStreamSynchronize(P.st[i])) != hipSuccess)
             return set_error(LDPC_EHIP, "decode_bits: %s", hipGetErrorString(e));
-    const int64_t nchunks = (rows + chunk - 1) / chunk;
-    // drain(slot, c): chunk c's bits have landed in h_bits[slot]: expand them to 0.0/1.0 doubles in `out`
-    auto drain = [&](int slot, int64_t c) -> int {
-        if ((e = hipEventSynchronize(P.done[slot])) != hipSuccess)
-            return set_error(LDPC_EHIP, "decode_bits chunk %lld: %s", (long long)c, hipGetErrorString(e));
-        const int64_t r0 = c * chunk, nr = std::min(chunk, rows - r0);
-        const uint8_t* hb = P.h_bits[slot];
-        parallel_rows(nr, threads, [&](int64_t a, int64_t b) {
-            const uint8_t* s = hb + a * n;
-            double* d = out + (r0 + a) * n;
-            for (int64_t i = 0, cnt = (b - a) * n; i < cnt; ++i) d[i] = (double)s[i];
-        });
-        return LDPC_OK;
-    };
-    // Two slots: while the GPU copies in / decodes / copies out chunk c on stream st[c&1], the host drains
-    // chunk c-2 and converts chunk c+1 into the other slot; the float64 -> float32 conversion (the
-    // reference's torch.tensor(..., dtype=torch.float), ofdm_functions.py:156) is fused into the staging
-    // copy, so PCIe carries 4 B per LLR in and 1 B per bit out.
-    for (int64_t c = 0; c < nchunks; ++c) {
-        const int slot = (int)(c & 1);
-        if (c >= 2 && (rc = drain(slot, c - 2)) != LDPC_OK) return rc;
-        const int64_t r0 = c * chunk, nr = std::min(chunk, rows - r0);
-        float* hl = P.h_llr[slot];
-        parallel_rows(nr, threads, [&](int64_t a, int64_t b) {
-            const double* s = llr + (r0 + a) * n;
-            float* d = hl + a * n;
-            for (int64_t i = 0, cnt = (b - a) * n; i < cnt; ++i) d[i] = (float)s[i];
-        });
-        hipStream_t st = P.st[slot];
-        if ((e = hipMemcpyAsync(P.d_llr[slot], hl, (size_t)nr * n * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
-            return set_error(LDPC_EHIP, "decode_bits H2D: %s", hipGetErrorString(e));
-        rc = decode_impl(g, P.d_llr[slot], nr, &q, P.d_bits[slot], nullptr, nullptr, P.d_ws[slot], P.ws_bytes, st,
-                         nullptr);
-        if (rc != LDPC_OK) return rc;
-        if ((e = hipMemcpyAsync(P.h_bits[slot], P.d_bits[slot], (size_t)nr * n, hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return set_error(LDPC_EHIP, "decode_bits D2H: %s", hipGetErrorString(e));
-        if ((e = hipEventRecord(P.done[slot], st)) != hipSuccess)
-            return set_error(LDPC_EHIP, "decode_bits event: %s", hipGetErrorString(e));
-    }
-    for (int64_t c = std::max<int64_t>(0, nchunks - 2); c < nchunks; ++c)
-        if ((rc = drain((int)(c & 1), c)) != LDPC_OK) return rc;
-    return LDPC_OK;
+    // the engine of the two-slot staging pipeline (host_pipeline.h): H2D, decode, D2H and a completion
+    // event per slot on that slot's stream
+    struct HipEngine {
+        ldpc_graph* g;
+        ldpc_graph::Pipe& P;
+        const ldpc_params* q;
+        int n;
+        float* h_llr(int s) { return P.h_llr[s]; }
+        const uint8_t* h_bits(int s) { return P.h_bits[s]; }
+        int submit(int s, int64_t nr) {
+            hipError_t e;
+            hipStream_t st = P.st[s];
+            if ((e = hipMemcpyAsync(P.d_llr[s], P.h_llr[s], (size_t)nr * n * 4, hipMemcpyHostToDevice, st)) != hipSuccess)
+                return set_error(LDPC_EHIP, "decode_bits H2D: %s", hipGetErrorString(e));
+            const int rc = decode_impl(g, P.d_llr[s], nr, q, P.d_bits[s], nullptr, nullptr, P.d_ws[s], P.ws_bytes, st,
+                                       nullptr);
+            if (rc != LDPC_OK) return rc;
+            if ((e = hipMemcpyAsync(P.h_bits[s], P.d_bits[s], (size_t)nr * n, hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return set_error(LDPC_EHIP, "decode_bits D2H: %s", hipGetErrorString(e));
+            if ((e = hipEventRecord(P.done[s], st)) != hipSuccess)
+                return set_error(LDPC_EHIP, "decode_bits event: %s", hipGetErrorString(e));
+            return LDPC_OK;
+        }
+        int wait(int s) {
+            const hipError_t e = hipEventSynchronize(P.done[s]);
+            return e == hipSuccess ? LDPC_OK : set_error(LDPC_EHIP, "decode_bits: %s", hipGetErrorString(e));
+        }
+    } eng{g, P, &q, n};
+    return staging_pipeline(eng, llr, rows, n, chunk, threads, out);
 }
 
 int ldpc_count_errors(const uint8_t* bits, const uint8_t* ref, int64_t B, int32_t n, int32_t info_bits, int64_t* counts,

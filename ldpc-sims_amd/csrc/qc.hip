@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
     // ds_bpermute sources then either coincide with an active lane's source (LDS broadcast) or fall on
     // banks no active lane uses; with their own bases they caused ~1.7 bank-conflict cycles per
     // bpermute (SQ_LDS_BANK_CONFLICT).
-    const int zb = (z < Z) ? z : z - Z;
+    const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
     // Lane frames (qc_tables.h PHI): lane z holds variable (j, (z + PHI[j]) mod Z); check labels are
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
                 if constexpr (s == 0) {
                     g[t] = app[j];
                 } else {
-                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(base4, base4m) + 4 * s;
+                    const int addr = sel_lanes<wrap_mask<Z, CPW>(Z - s)>(base4, base4m) + 4 * s;
                     g[t] = bperm(addr, app[j]);
                 }
             });
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
                 if constexpr (s == 0) {
                     cr[t] = c;
                 } else {
-                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
+                    const int addr = sel_lanes<wrap_mask<Z, CPW>(s)>(base4, base4m) + 4 * (Z - s);
                     cr[t] = bperm(addr, c);
                 }
             });
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t cw = wave * CPW + half;
     const bool valid = (z < Z) && (cw < B);
-    const int zb = (z < Z) ? z : z - Z;
+    const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
     // lane rotations through a per-wave LDS row instead of ds_bpermute (see QC_PH_LDSROT)
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
                 if constexpr (s == 0) {
                     x = msg[e0 + t];
                 } else {
-                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(base4, base4m) + 4 * s;
+                    const int addr = sel_lanes<wrap_mask<Z, CPW>(Z - s)>(base4, base4m) + 4 * s;
                     x = xfer(addr, msg[e0 + t]);
                 }
                 v[t] = x;
@@ -504,7 +504,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
                 if constexpr (s == 0) {
                     cr = c;
                 } else {
-                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
+                    const int addr = sel_lanes<wrap_mask<Z, CPW>(s)>(base4, base4m) + 4 * (Z - s);
                     cr = xfer(addr, c);
                 }
                 msg[e0 + t] = cr;
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t cw = wave * CPW + half;
     const bool valid = (z < Z) && (cw < B);
-    const int zb = (z < Z) ? z : z - Z;
+    const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
     using f4 = __attribute__((ext_vector_type(4))) float;
@@ -652,7 +652,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
         constexpr int rho = decltype(rr)::value;
         if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES)
-            ra[rho] = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho;
+            ra[rho] = sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho;
     });
     auto rot = [&](auto rr, float x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
         constexpr int rho = decltype(rr)::value;
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         } else if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES) {
             return xfer(ra[rho], x);
         } else {
-            return xfer(sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho, x);
+            return xfer(sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho, x);
         }
     };
     (void)ra;
@@ -837,7 +837,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         constexpr int rho = decltype(rr)::value;
         int addr;
         if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES) addr = ra[rho];
-        else addr = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho;
+        else addr = sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho;
         return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Rw) + addr);
     };
     auto back_col = [&](auto pp, float* T) __attribute__((always_inline)) {  // c2v of column lcol(p), variable frame
@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t cw = wave * CPW + half;
     const bool valid = (z < Z) && (cw < B);
-    const int zb = (z < Z) ? z : z - Z;
+    const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
     // lane rotations through a per-wave LDS row instead of ds_bpermute (see QC_PH_LDSROT)
@@ -1166,7 +1166,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 if constexpr (s == 0) {
                     g[t] = msg[e0 + t];
                 } else {
-                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(Z - s, Z)>(base4, base4m) + 4 * s;
+                    const int addr = sel_lanes<wrap_mask<Z, CPW>(Z - s)>(base4, base4m) + 4 * s;
                     g[t] = xfer(addr, msg[e0 + t]);
                 }
             });
@@ -1177,7 +1177,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 if constexpr (s == 0) {
                     msg[e0 + t] = g[t];
                 } else {
-                    const int addr = sel_lanes<lane_range_mask<Z, CPW>(s, Z)>(base4, base4m) + 4 * (Z - s);
+                    const int addr = sel_lanes<wrap_mask<Z, CPW>(s)>(base4, base4m) + 4 * (Z - s);
                     msg[e0 + t] = xfer(addr, g[t]);
                 }
             });

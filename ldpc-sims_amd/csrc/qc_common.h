@@ -173,6 +173,40 @@ constexpr uint64_t lane_range_mask(int lo, int hi) {
     return m;
 }
 
+// Which lane's slot an idle lane (z >= Z) reads in a rotation.  ds_bpermute and ds_read_b32 serve a wave in
+// two 32-lane halves with bank = (address / 4) mod 32; an identical address within a half is a broadcast, a
+// second distinct address on a bank one extra LDS cycle.  With one codeword per wave (CPW == 1, 32 < Z < 64)
+// the idle lanes 54..63 of Z = 54 sit in the upper half; aliased to lifting index z - Z (round 2) they read
+// lanes just above 0..9's sources — a distinct address on a bank the wrapped active lanes use, exactly one
+// extra cycle per rotation on every (1296,2/3) rotation (modelled: 104 of 104; measured SQ_LDS_BANK_CONFLICT
+// = SQ_INSTS_LDS).  QC_IDLE_ALIAS: alias them to an active lane of the SAME half instead (z' = 32 + (z - Z)
+// mod (Z - 32)), wrap decision included, so they repeat its address exactly: 0.62 extra cycles per rotation
+// (the rest are the active lanes' own wrap collisions).  CPW == 2 (Z <= 32) is conflict-free either way.
+#ifndef QC_IDLE_ALIAS
+#define QC_IDLE_ALIAS 1
+#endif
+template <int Z, int CPW>
+constexpr int idle_alias(int z) {  // z >= Z: the lifting index whose rotation addresses this idle lane repeats
+    if constexpr (QC_IDLE_ALIAS && CPW == 1 && Z > 32) return 32 + (z - Z) % (Z - 32);
+    else return z - Z;
+}
+template <int Z, int CPW>
+__device__ __forceinline__ int lane_zb(int z) {
+    return (z < Z) ? z : idle_alias<Z, CPW>(z);
+}
+// lanes that take the wrapped address of a rotation whose source z + rho reaches Z: z in [lo, Z), and idle
+// lanes whose alias is
+template <int Z, int CPW>
+constexpr uint64_t wrap_mask(int lo) {
+    uint64_t m = lane_range_mask<Z, CPW>(lo, Z);
+    if (CPW == 1)
+        for (int l = Z; l < 64; ++l) {
+            const int a = idle_alias<Z, CPW>(l);
+            if (a >= lo && a < Z) m |= 1ull << l;
+        }
+    return m;
+}
+
 // lane in MASK ? b : a.  The mask is a compile-time SGPR-pair constant, so the select is one VALU op
 // with no v_cmp (and no VCC hazard).  Volatile: never CSE'd across rows or hoisted out of the loop.
 template <uint64_t MASK>

@@ -49,6 +49,9 @@ namespace ldpc {
 #ifndef QC_PK_ADDR_MIN_USES_Z64
 #define QC_PK_ADDR_MIN_USES_Z64 4  // Z > 32 (one lane group): 6 address registers at 4 uses (18 at 3)
 #endif
+#ifndef QC_PK_ES_ROWS
+#define QC_PK_ES_ROWS 1  // early-stop syndrome row by row with an early exit (one codeword pair per wave, Z = 54)
+#endif
 #ifndef QC_PK_TPB
 #define QC_PK_TPB 256
 #endif
@@ -123,7 +126,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     const int z = (CPW == 2) ? (lane & 31) : lane;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t cw0 = (wave * CPW + half) * 2;  // low fp16: cw0, high: cw0 + 1
-    const int zb = (z < Z) ? z : z - Z;
+    const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
     using f4 = __attribute__((ext_vector_type(4))) float;
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
         constexpr int rho = decltype(rr)::value;
         if constexpr (rot_uses<C>(rho) >= MINU)
-            ra[rho] = sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho;
+            ra[rho] = sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho;
     });
     auto rot = [&](auto rr, uint32_t x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
         constexpr int rho = decltype(rr)::value;
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
         } else if constexpr (rot_uses<C>(rho) >= MINU) {
             return xfer(ra[rho], x);
         } else {
-            return xfer(sel_lanes<lane_range_mask<Z, CPW>(Z - rho, Z)>(rb4, rb4m) + 4 * rho, x);
+            return xfer(sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho, x);
         }
     };
     (void)ra;
@@ -268,29 +271,55 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
                 constexpr int p = decltype(pp)::value;
                 app[lcol<C>(p)] = vn_col(pp);
             });
-            // syndrome of APP_{it+1} per fp16 half k (one codeword per lane group each): per block column one
-            // ballot of the hard decisions (oracle: bit = APP < 0), rotated into each check's frame and XOR-ed
-            uint32_t conv = 0;  // bit 2g + k: group g's codeword k satisfies every check
-            static_for<0, 2>([&](auto kk) __attribute__((always_inline)) {
-                constexpr int k = decltype(kk)::value;
-                uint64_t par[MB];
-#pragma unroll
-                for (int r = 0; r < MB; ++r) par[r] = 0;
-                static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
-                    constexpr int j = decltype(jj)::value;
-                    const uint64_t b = __ballot(as_h2(app[j])[k] < (_Float16)0) & ACTIVE;
-                    static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
-                        constexpr int r = decltype(rr)::value;
-                        constexpr int t = first_slot<C>(r, j);
-                        if constexpr (t >= 0) par[r] ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
-                    });
+            // syndrome of APP_{it+1}: bit 2g + k of `conv` = codeword k (fp16 half) of lane group g satisfies
+            // every check.  Per block column one ballot of the hard decisions (oracle: bit = APP < 0) per half,
+            // rotated into the frame of each row it touches and XOR-ed there.
+            uint32_t conv;
+            if constexpr (QC_PK_ES_ROWS && CPW == 1) {
+                // Row by row with an early exit (one codeword pair per wave, (1296,2/3)): `conv` starts as the
+                // codewords not yet done and loses each one whose row parity is nonzero; the scan stops once no
+                // codeword of the wave can still be satisfied — at low Eb/N0 after the first row, so the test
+                // costs about one row of scalar rotations instead of all MB.  The ballot is re-taken at every
+                // use (one v_cmp): holding 2 x NB of them spilled SGPRs.  The decision is unchanged.
+                conv = ALL & ~done;
+                static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                    constexpr int r = decltype(rr)::value;
+                    if (conv) {
+                        static_for<0, 2>([&](auto kk) __attribute__((always_inline)) {
+                            constexpr int k = decltype(kk)::value;
+                            uint64_t par = 0;
+                            static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                                constexpr int t = decltype(tt)::value;
+                                const uint64_t b = __ballot(as_h2(app[C::COL[r][t]])[k] < (_Float16)0) & ACTIVE;
+                                par ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                            });
+                            if (par & G0) conv &= ~(1u << k);
+                        });
+                    }
                 });
-                uint64_t u = 0;
+            } else {  // all rows at once (two codeword pairs per wave: the row-wise form spills 49 VGPRs there)
+                conv = 0;
+                static_for<0, 2>([&](auto kk) __attribute__((always_inline)) {
+                    constexpr int k = decltype(kk)::value;
+                    uint64_t par[MB];
 #pragma unroll
-                for (int r = 0; r < MB; ++r) u |= par[r];
-                conv |= ((u & G0) ? 0u : 1u) << k;
-                if constexpr (CPW == 2) conv |= ((u & G1) ? 0u : 1u) << (2 + k);
-            });
+                    for (int r = 0; r < MB; ++r) par[r] = 0;
+                    static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                        constexpr int j = decltype(jj)::value;
+                        const uint64_t b = __ballot(as_h2(app[j])[k] < (_Float16)0) & ACTIVE;
+                        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                            constexpr int r = decltype(rr)::value;
+                            constexpr int t = first_slot<C>(r, j);
+                            if constexpr (t >= 0) par[r] ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                        });
+                    });
+                    uint64_t u = 0;
+#pragma unroll
+                    for (int r = 0; r < MB; ++r) u |= par[r];
+                    conv |= ((u & G0) ? 0u : 1u) << k;
+                    if constexpr (CPW == 2) conv |= ((u & G1) ? 0u : 1u) << (2 + k);
+                });
+            }
             const uint32_t fresh = conv & ~done;
             if (fresh) {
                 if (fresh & 1u) used0 = it + 1;

@@ -209,6 +209,14 @@ constexpr uint64_t wrap_mask(int lo) {
 
 // lane in MASK ? b : a.  The mask is a compile-time SGPR-pair constant, so the select is one VALU op
 // with no v_cmp (and no VCC hazard).  Volatile: never CSE'd across rows or hoisted out of the loop.
+//
+// A mask whose upper 33 bits are all ones (the sign extension of a negative 32-bit value: e.g. lanes 19..63 of
+// a Z = 54 wrap mask with aliased idle lanes) is materialised by the ROCm 7.2 compiler as
+// `s_mov_b64 s[..], <32-bit literal>`, which the gfx950 SALU ZERO-extends (measured: every (1296,2/3)
+// register kernel decoded garbage; the compiler itself emits `s_mov_b64 s[..], 0xffffffff` for the 64-bit
+// value 0x00000000ffffffff elsewhere).  Such masks are passed complemented, with the operands swapped: the
+// complement's upper bits are zero, a value either extension reads the same.  tests/test_kernel_resources.py
+// checks the built code for 64-bit SALU moves of high-bit literals.
 template <uint64_t MASK>
 __device__ __forceinline__ int sel_lanes(int a, int b) {
 #if QC_DIAG_NOSEL
@@ -216,7 +224,10 @@ __device__ __forceinline__ int sel_lanes(int a, int b) {
     return a;
 #else
     int r;
-    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(MASK));
+    if constexpr ((MASK >> 31) == 0x1FFFFFFFFull)
+        asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(~MASK));
+    else
+        asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(MASK));
     return r;
 #endif
 }

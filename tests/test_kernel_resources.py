@@ -100,3 +100,18 @@ def test_lds_row_rotation_kernels_write_m0_once():
         assert len(m0) == 1 and m0[0].startswith("s_mov_b32 m0,"), (k, m0)
     head = "_ZN4ldpc10k_qc_ms_phINS_10Wifi648_12ELb0ELb0ELi0EEEvPKfliffffffiPhPfPi"
     assert sum("ds_write_addtid_b32" in i for i in rot[head]) >= 88, "LDS-row rotations missing"
+
+
+def test_no_sign_extended_64bit_salu_literals():
+    """64-bit SALU moves of a 32-bit literal with bit 31 set: the gfx950 SALU zero-extends the literal, so such a
+    move is only right when the intended value is the zero extension.  The one legitimate use in the library is
+    0xffffffff (a ballot's low half, 0x00000000ffffffff); any other (the compiler lowering a sign-extended
+    64-bit lane mask that way — it decoded garbage in every Z = 54 kernel) fails here.  qc_common.h sel_lanes
+    passes such masks complemented."""
+    pat = re.compile(r"^\s*s_\w+_b64\s+[^/]*?(0x[89a-fA-F][0-9a-fA-F]{7})\b")
+    bad = {}
+    for k, insts in _kernel_bodies().items():
+        hits = [i for i in insts if (m := pat.match(i)) and m.group(1).lower() != "0xffffffff"]
+        if hits:
+            bad[k] = hits[:3]
+    assert not bad, bad

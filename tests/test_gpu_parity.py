@@ -297,8 +297,8 @@ def test_degenerate_graph_empty_row_and_column():
         assert np.array_equal(r["bits"], ref["bits"])
 
 
-@pytest.mark.parametrize("name,B,iters", [("dvbs2_12", 32, 50), ("dvbs2s_12", 6, 12)])
-def test_dvbs2_minsum_bit_exact_and_sp_bits(name, B, iters):
+@pytest.mark.parametrize("name,B,iters,ebn0", [("dvbs2_12", 32, 50, 0.9), ("dvbs2s_12", 6, 12, 3.0)])
+def test_dvbs2_minsum_bit_exact_and_sp_bits(name, B, iters, ebn0):
     """BASELINE config [4]'s code (EN 302 307 rate 1/2, codes.dvbs2_12) at its 50 iterations on 32 codewords,
     and the shaped stand-in: min-sum bits and z bitwise vs the oracle (plain min-sum as config [4] runs it, and
     normalised), tanh-SP bits identical and z within the oracle tolerance; the reference cannot instantiate
@@ -307,7 +307,7 @@ def test_dvbs2_minsum_bit_exact_and_sp_bits(name, B, iters):
     c, _ = get_code(name)
     rng = np.random.default_rng(9)
     cw = IRAEncoder(c).encode(rng.integers(0, 2, size=(B, c.k)))
-    sigma = np.sqrt(1.0 / (2 * 0.5 * 10 ** (0.9 / 10)))   # the waterfall: some codewords converge, some do not
+    sigma = np.sqrt(1.0 / (2 * 0.5 * 10 ** (ebn0 / 10)))  # EN 302 307 at 0.9 dB: in the waterfall (31/32 decode)
     llr = (-2.0 * ((1.0 - 2.0 * cw) + sigma * rng.standard_normal(cw.shape)) / sigma**2).astype(np.float32)
     dec = ldpc_amd.get_decoder(c)
     x = torch.from_numpy(llr).cuda()

@@ -39,7 +39,7 @@ void k_qc_ms_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     const int64_t cw = (int64_t)blockIdx.x * 2 + h;
     const bool live = l < ZL;
     const bool valid = live && cw < B;
-    const int zc = live ? l + ZL * k : 0;
+    const int zc = live ? l + ZL * k : (QC_SL_IDLE_ALIAS ? ZL * k : 0);  // idle lanes: see qc_sl_sp.h
     const int xb = h * 2 * Z + zc;
     float Lr[NB], app[NB];
     {

@@ -51,6 +51,9 @@ constexpr int nz_max() {
 // buffer).  QC_SL_SP_L: where L lives — 0 VGPRs, 1 LDS, 2 re-read from global memory (an L2 hit) at every
 // use.  Fixed-count kernel: one buffer + L in global = 26 KB of LDS per unit, 112 VGPRs: five units
 // (15 waves) per CU instead of two.
+#ifndef QC_SL_IDLE_ALIAS
+#define QC_SL_IDLE_ALIAS 1  // idle lanes read at their wave's first position (0: at position 0, round 2)
+#endif
 #ifndef QC_SL_SP_SERIAL_CN
 #define QC_SL_SP_SERIAL_CN 1
 #endif
@@ -90,7 +93,11 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     const int64_t cw = (int64_t)blockIdx.x * 2 + h;
     const bool live = l < ZL;                // lane carries a frame position
     const bool valid = live && cw < B;       // ... of a real codeword
-    const int zc = live ? l + ZL * k : 0;    // idle lanes alias position 0 for reads (never store)
+    // idle lanes (l >= ZL) alias this wave's first position for reads (they never store): an exchange read is
+    // served per 32-lane half with bank = (address / 4) mod 32, and aliased to position 0 (round 2) the idle
+    // lanes of waves k = 1, 2 read a distinct address on a bank their active lanes use — one extra LDS cycle
+    // per read; repeating an active lane's address of their own wave is a broadcast instead.
+    const int zc = live ? l + ZL * k : (QC_SL_IDLE_ALIAS ? ZL * k : 0);
     const int xb = h * 2 * Z + zc;           // this lane's position in an exchange row
     // L = -llr (bp.py:47) of this lane's variable in every block column
     const float* const lp = llr + (valid ? cw * N : 0);

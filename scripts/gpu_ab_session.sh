@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round-3: GPU tests, the bench line, A/B of the idle-lane aliasing (Z = 54 packed, Z = 81 sliced), drop-in sweep,
-# config [2] profile.
+# GPU tests, the bench line, an A/B of library variants (round 3: the idle-lane aliasing, Z = 54 packed and
+# Z = 81 sliced), the drop-in sweep and a config [2] profile, on one box.  OUT=gpurun_out/<name> bash scripts/gpu_ab_session.sh
+
 set -o pipefail
-OUT=${OUT:-gpurun_out/r3e}; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=${OUT:-gpurun_out/ab_session}; mkdir -p $OUT; export TMPDIR=/tmp
 LDPC_PARITY_LOG=$OUT/soft_parity.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail $OUT/bench.err; exit 1; }

@@ -118,16 +118,12 @@ __device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
 // caller's clamp (bp.py:47); its sign the xor of the others' signs.
 constexpr float kRmaxF32 = 16777215.0f;
 
-// exp(-|x|) with the device library's split log2(e) product (as tanh_f32 above), then the sign of x
+// exp(-|x|) as one v_exp_f32 of the rounded product -|x| * log2(e), with the sign of x.  The oracle's (D, S)
+// form computes the same expression (exp2f of the same fp32 product); the split-log2(e) product of the device
+// library's expf (tanh_f32 above) is not needed here: a relative error of |x| * 2^-24 in a moves the check
+// output log(S/D) by at most that much absolutely, and |x| beyond the clamp leaves it saturated.
 __device__ __forceinline__ float vn_signed_a(float x) {
-    const float t = fminf(fabsf(x), 104.0f);               // exp(-104) < 2^-149: 0 (or a flushed denormal) either way
-    const float ph = t * -0x1.715476p+0f;                  // -|x| * log2(e)
-    const float n = __builtin_rintf(ph);
-    float lo = __builtin_fmaf(t, -0x1.715476p+0f, -ph);
-    lo = __builtin_fmaf(t, -0x1.4ae0bep-26f, lo);
-    const float f = (ph - n) + lo;
-    const float e = __builtin_ldexpf(__builtin_amdgcn_exp2f(f), (int)n);
-    return __builtin_copysignf(e, x);
+    return __builtin_copysignf(__builtin_amdgcn_exp2f(fabsf(x) * -0x1.715476p+0f), x);
 }
 
 struct DSet {
@@ -141,7 +137,7 @@ __device__ __forceinline__ DSet ds_push(DSet x, float a) {  // a = |signed a| of
 __device__ __forceinline__ float ds_out(float D, float S, uint32_t sgn, float clamp) {
     float r = S * __builtin_amdgcn_rcpf(D);                    // D == 0: +inf -> RMAX
     r = __builtin_amdgcn_fmed3f(r, 1.0f, kRmaxF32);
-    const float y = fminf(log_f32_normal(r), clamp);
+    const float y = fminf(__builtin_amdgcn_logf(r) * 0x1.62e430p-1f, clamp);  // ln r = log2(r) * ln 2 (fp32 product)
     return u2f(f2u(y) | (sgn & 0x80000000u));
 }
 // the output of an edge from its prefix set p and suffix set q (the join, then ds_out)

@@ -77,7 +77,8 @@ static int syndrome_ok(const graph_t* g, const uint8_t* bits);
  * |p| = |prod tanh| = (S-D)/(S+D) and log((1+|p|)/(1-|p|)) = log(S/D).  Adding one edge (a, 1):
  * D' = D + a*S, S' = S + a*D; joining two sets: D = Dp*Sq + Sp*Dq, S = Sp*Sq + Dp*Dq — sums of positive
  * terms only, so every step is accurate to an ulp, where the reference's fp32 form loses digits near |p| -> 1
- * (1-p cancels; one ulp of tanh near 1 is a 1e-4..1e-3 error in log).  Exclusive (D, S) per edge from prefix
+ * (1-p cancels; one ulp of tanh near 1 is a 1e-4..1e-3 error in log).  a = exp2(fp32(-|s| * log2 e)) and
+ * ln r = fp32(log2(r) * ln 2), one transcendental each, as the GPU computes them.  Exclusive (D, S) per edge from prefix
  * and suffix sets, O(d) per check.  The clamp |p| <= 1-1e-7 is S/D <= RMAX = (1+pmax)/(1-pmax) (fp32:
  * 16777215 = the reference's fp32 bound exactly), then the caller's clamp; sign = xor of the others' signs.
  * An s of +-0 gives a = 1, whose set has D == S exactly (the symmetric join keeps it so): log 1 = 0 for the
@@ -87,7 +88,7 @@ static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float 
                           float* sufD, float* sufS) {
     if (d == 0) return;  /* an empty check (all-zero row of H) has no edges */
     if (d == 1) {  /* empty product = 1 -> the p clamp */
-        const float y = logf(RMAX_F32);
+        const float y = log2f(RMAX_F32) * 0.693147182f;
         out[0] = y > clamp ? clamp : y;
         return;
     }
@@ -108,7 +109,7 @@ static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float 
         else { D = pD * sufS[t + 1] + pS * sufD[t + 1]; S = pS * sufS[t + 1] + pD * sufD[t + 1]; }
         float r = S / D;                      /* D == 0 (every other a underflowed): +inf -> RMAX */
         if (!(r <= RMAX_F32)) r = RMAX_F32;
-        float y = logf(r);
+        float y = log2f(r) * 0.693147182f;  /* ln r as log2(r) * ln 2 in fp32, as the GPU */
         if (y > clamp) y = clamp;
         out[t] = u2f(f2u(y) | ((sg ^ f2u(sa[t])) & 0x80000000u));
         const float a = fabsf(sa[t]);
@@ -147,7 +148,7 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
                     if (u != t) S += wv ? wv[(t - a) * d + (u - a)] * x[g->var_edges[u]] : x[g->var_edges[u]];
                 if (stable) {  /* signed a = copysign(exp(-|s|), s), s = 2 * the reference's tanh argument */
                     const float sv = Lw + S;
-                    v2c[g->var_edges[t]] = copysignf(expf(-fabsf(sv)), sv);
+                    v2c[g->var_edges[t]] = copysignf(exp2f(fabsf(sv) * -1.44269502f), sv);  /* fp32 product, as the GPU */
                 } else {
                     v2c[g->var_edges[t]] = tanhf(0.5f * (Lw + S));
                 }

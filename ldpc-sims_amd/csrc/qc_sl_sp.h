@@ -75,6 +75,13 @@ constexpr int nz_max() {
 #define QC_SL_SP_LPF 0  // A/B: 1.874 vs 1.887 M cw/s, -0.8 % (profiles/r02/ab/ab_lpf.txt): the other waves hide it
 #endif
 
+#ifndef QC_SL_DIAG_NOBAR
+#define QC_SL_DIAG_NOBAR 0  // DIAGNOSTIC BUILD ONLY (wrong results): no row-exchange barriers, to price them
+#endif
+__device__ __forceinline__ void sl_barrier() {
+    if constexpr (!QC_SL_DIAG_NOBAR) __syncthreads();
+}
+
 template <class C, bool EARLY>
 __global__ __launch_bounds__(C::S * 64)
 __attribute__((amdgpu_waves_per_eu(EARLY ? QC_SL_SP_WAVES_PER_SIMD_EARLY : QC_SL_SP_WAVES_PER_SIMD)))
@@ -257,7 +264,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                     }
                 });
             }
-            __syncthreads();
+            sl_barrier();
             float g[d];
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
@@ -266,7 +273,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 else g[t] = Xv[nz_index<C>(r, t) * ROW + xb + s];
             });
             cn_ds_row<d, QC_SL_SP_SERIAL_CN != 0>(g, clamp);  // O(d) exclusive sets (common.h)
-            if constexpr (CMP) __syncthreads();  // every wave has read this row's v2c before the buffer takes its c2v
+            if constexpr (CMP) sl_barrier();  // every wave has read this row's v2c before the buffer takes its c2v
             if (live) {
                 static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                     constexpr int t = decltype(tt)::value;
@@ -277,14 +284,14 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                     }
                 });
             }
-            __syncthreads();
+            sl_barrier();
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int s = C::SHR[r][t];
                 if constexpr (s == 0) msg[e0 + t] = g[t];
                 else msg[e0 + t] = Xc[nz_index<C>(r, t) * ROW + xb + (Z - s)];
             });
-            if constexpr (CMP) __syncthreads();  // ... and its c2v before the next row's v2c lands in the buffer
+            if constexpr (CMP) sl_barrier();  // ... and its c2v before the next row's v2c lands in the buffer
         });
     }
     if (EARLY && (h ? done1 : done0)) {

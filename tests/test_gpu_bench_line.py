@@ -1,0 +1,37 @@
+"""The bench.py JSON line (the driver's contract, BASELINE.json metric) on a short run: every field the
+round's records rely on is present and consistent — the value from the step time, the roofline with its
+counters, the CPU baselines (the C port timed here and the reference's own CPU record, never silently
+dropped), the side measurements, the rank evidence and the BER curve."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_line_contract():
+    out = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--batch", "8192",
+                          "--cpu-seconds", "0.5"], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert d["unit"] == "codewords/s" and d["higher_is_better"] is True and d["n_gpus"] == 1
+    assert abs(d["value"] - 8192 / (d["ms_per_step"] / 1e3)) <= 1e-6 * d["value"]
+    roof = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in roof
+    assert roof["bound"] in ("lds", "valu", "hbm") and roof["frac"] > 0
+    cpu = d["cpu_baseline"]
+    assert cpu["kind"] == "port" and cpu["value"] > 0 and cpu["cores"] >= 1
+    ref = cpu["reference"]
+    assert ref["kind"] == "reference" and "missing" not in ref, ref
+    assert ref["value"] > 0 and ref["gpu_tanh_sp_over_reference"] > 1e5 and ref["dropin_over_reference"] > 1e4
+    assert d["side"]["gpu_tanh_sp"]["cw_per_s"] > 0 and d["dropin_cw_per_s"] > 0
+    assert d["ranks"]["world_size"] == 1 and len(d["ranks"]["per_rank"]) == 1
+    assert len(d["ber"]["ebn0_db"]) == 11 and d["ber"]["codewords_per_point"] == 8192

@@ -535,3 +535,20 @@ def test_decode_llr_sign_convention():
     assert np.array_equal(a, b) and np.array_equal(a, c)
     with pytest.raises(ValueError):
         ldpc_amd.decode(H, llr, 10, llr_sign="bogus")
+
+
+@pytest.mark.parametrize("code", ["peg64_32", "wifi648_12", "wifi1296_23", "wifi1944_56"])
+def test_tanh_zero_llr_rows_exact(code, force_generic):
+    """All-zero LLR rows through tanh-SP (register / sliced and generic kernels): the reference gives z = 0
+    exactly (tanh(0) = 0 zeroes every product; p1 = 0.5 rounds to bit 0); the (D, S) form keeps D == S
+    exactly for a = 1, so the GPU must return exact zeros too, and equal the oracle's bits elsewhere."""
+    H, _ = get_code(code)
+    rate = 1 - H.shape[0] / H.shape[1]
+    cw, llr = _llr(H, 130, 1.5 if rate < 0.6 else 3.5, seed=77, rate=rate)
+    llr[:3] = 0.0
+    dec = ldpc_amd.get_decoder(H)
+    r = dec.decode(torch.from_numpy(llr).cuda(), 12, algo="tanh", clamp=10.0, soft="z", force_generic=force_generic)
+    z = r["soft"].cpu().numpy()
+    assert np.all(z[:3] == 0.0) and not r["bits"][:3].cpu().numpy().any()
+    ref = oracle.sp_f32(H, llr, 12, 10.0, stable=True)
+    assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])

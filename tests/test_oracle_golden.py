@@ -193,3 +193,19 @@ def test_degenerate_graph_both_forms():
     b = oracle.sp_f32(H, llr, 7, 20.0, stable=True)
     assert np.array_equal(a["bits"], b["bits"])
     assert np.allclose(a["z"], b["z"], rtol=1e-4, atol=1e-4)
+
+
+def test_zero_llr_rows_give_exact_zero_in_both_forms():
+    """An all-zero LLR row: the reference's v2c tanh(0) = 0 makes every product 0 and every c2v log(1) = 0, so
+    z = 0 exactly and p1 = 0.5 (np.round -> 0).  The (D, S) form: a = 1 for every edge keeps D == S in every
+    set, log(S/D) = 0 exactly — the same zeros, not merely small values."""
+    H = np.array(np.load(os.path.join(GOLDEN, "peg64_32.npz"))["H"])
+    llr = np.zeros((3, 64), np.float32)
+    llr[1, ::2] = 2.5                      # half zeros: the zero variables' checks still see exact zeros
+    for stable in (False, True):
+        r = oracle.sp_f32(H, llr, 10, 10.0, stable=stable)
+        assert np.all(r["z"][0] == 0.0) and np.all(r["p1"][0] == 0.5) and not r["bits"][0].any()
+    a = oracle.sp_f32(H, llr, 10, 10.0)
+    b = oracle.sp_f32(H, llr, 10, 10.0, stable=True)
+    assert np.array_equal(a["bits"], b["bits"])
+    assert np.allclose(a["z"], b["z"], rtol=1e-5, atol=1e-6)

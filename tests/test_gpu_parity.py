@@ -552,3 +552,22 @@ def test_tanh_zero_llr_rows_exact(code, force_generic):
     assert np.all(z[:3] == 0.0) and not r["bits"][:3].cpu().numpy().any()
     ref = oracle.sp_f32(H, llr, 12, 10.0, stable=True)
     assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])
+
+
+@pytest.mark.parametrize("name,iters", [("wifi648_12", 50), ("wifi1296_23", 20), ("wifi1944_56", 10)])
+def test_decode_bits_dropin_long_reference_goldens(name, iters):
+    """The drop-in itself (decode_bits from host float64, ofdm_functions.py:131-163) on the reference runs at
+    the drop-in's / BASELINE configs' iteration counts: every decoded row's bits equal the reference's fp32
+    decode_bits bits (np.round(p1)); the ragged tail (N % batch_size) stays 0."""
+    from ldpc_amd.codes import qc_expand
+    d = np.load(os.path.join(GOLDEN, f"bp_{name}_sp_it{iters}.npz"))
+    H = qc_expand(d["base"], int(d["Z"]))
+    for snr in d["snrs"]:
+        tag = f"snr{snr:g}".replace(".", "p")
+        llr = d[f"llr_{tag}"].astype(np.float64)
+        bs = max(1, llr.shape[0] // 3)
+        out = ldpc_amd.decode_bits(llr, H, iters, bs, float(d["clamp"]))
+        rows = (llr.shape[0] // bs) * bs
+        assert out.dtype == np.float64
+        assert np.array_equal(out[:rows], np.round(d[f"p1_f32_{tag}"][:rows]).astype(np.float64))
+        assert not out[rows:].any()

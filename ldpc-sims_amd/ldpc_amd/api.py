@@ -247,6 +247,54 @@ def decode(H, llr, max_iters: int, *, algo="tanh", clamp=10.0, alpha=1.0, beta=0
     return r
 
 
+class _OutputPool:
+    """Recycled float64 output buffers for ``decode_bits``.
+
+    The reference's contract returns a fresh (N, n) float64 array per call (``ofdm_functions.py:133``); the
+    host cost of a fresh 340 MB array is populating its pages (14-26 ms on the GPU box, more than the whole
+    decode — DESIGN.md §9).  A returned array is an ordinary numpy array over a pooled buffer; when the caller
+    drops it (and every view of it), a ``weakref.finalize`` on its per-call buffer exporter puts the buffer
+    back, and a later call of the same size reuses it: the library rewrites every decoded row and the tail
+    rows are zeroed, so each result is indistinguishable from a fresh ``np.zeros`` one.  At most ``keep`` free
+    buffers of at most ``max_bytes`` in total are held (the oldest are released first)."""
+
+    def __init__(self, keep=2, max_bytes=2 << 30):
+        self.keep, self.max_bytes = keep, max_bytes
+        self._free = []          # [(nbytes, 1-D float64 buffer)], oldest first
+        self._lock = threading.Lock()
+
+    def _release(self, buf):
+        with self._lock:
+            self._free.append((buf.nbytes, buf))
+            while len(self._free) > self.keep or sum(b for b, _ in self._free) > self.max_bytes:
+                self._free.pop(0)
+
+    def array(self, shape, rows):
+        """(shape) float64 array whose rows >= ``rows`` are zero; rows < ``rows`` are for the caller to fill."""
+        import weakref
+        count = int(np.prod(shape))
+        buf = None
+        with self._lock:
+            for i, (nb, b) in enumerate(self._free):
+                if b.size == count:
+                    buf = self._free.pop(i)[1]
+                    break
+        if buf is None:
+            if count * 8 > self.max_bytes:
+                return np.zeros(shape)
+            buf = np.empty(count)
+        # the returned array (and every view of it) bottoms out in a per-call ctypes exporter of the pooled
+        # memory: numpy collapses view chains onto the exporter, so it dies only with the last view
+        holder = (ctypes.c_double * count).from_address(buf.ctypes.data)
+        weakref.finalize(holder, self._release, buf)
+        out = np.frombuffer(holder, dtype=np.float64).reshape(shape)
+        out[rows:] = 0.0
+        return out
+
+
+_outputs = _OutputPool()
+
+
 def decode_bits(llrs, H, bp_iterations, batch_size, clamp_value):
     """Drop-in for ``decode_bits`` (``pytorch/ofdm/ofdm_functions.py:131-163``).
 
@@ -256,11 +304,14 @@ def decode_bits(llrs, H, bp_iterations, batch_size, clamp_value):
     ``(N // batch_size) * batch_size`` rows are decoded and the remainder stays 0 (``:133-135``).
     """
     llrs = np.asarray(llrs)
-    output_bits = np.zeros(llrs.shape)
     num_batches = llrs.shape[0] // batch_size  # ZeroDivisionError for batch_size == 0, as the reference
     rows = num_batches * batch_size
-    if rows == 0:
-        return output_bits
+    if rows == 0 or llrs.ndim != 2:
+        output_bits = np.zeros(llrs.shape)
+        if rows == 0:
+            return output_bits
+    else:
+        output_bits = _outputs.array(llrs.shape, rows)  # rows >= `rows` zero; the library writes the rest
     hshape = H.shape if isinstance(H, SparseCode) else np.asarray(H).shape
     if llrs.ndim != 2 or llrs.shape[1] != hshape[1]:
         raise RuntimeError(f"llrs shape {llrs.shape} does not match H {hshape}")

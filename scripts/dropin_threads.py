@@ -29,14 +29,16 @@ def main():
     dec = ldpc_amd.get_decoder(H)
     p = dec.params(50, "tanh", 10.0)
     # the drop-in itself (fresh np.zeros output per call, as the reference's decode_bits), steady state
-    ldpc_amd.decode_bits(llr, H, 50, 256, 10.0)
-    ts = []
-    for _ in range(3):
-        t = time.perf_counter()
-        ldpc_amd.decode_bits(llr, H, 50, 256, 10.0)
-        ts.append(time.perf_counter() - t)
-    print(json.dumps({"what": "decode_bits (fresh output)", "best_s": min(ts), "mean_s": sum(ts) / 3,
-                      "cw_per_s": B / (sum(ts) / 3)}), flush=True)
+    for what, keep in (("decode_bits, result dropped each call", False), ("decode_bits, bits = ... loop", True)):
+        r = None
+        ts = []
+        for _ in range(5):
+            t = time.perf_counter()
+            x = ldpc_amd.decode_bits(llr, H, 50, 256, 10.0)
+            ts.append(time.perf_counter() - t)
+            r = x if keep else None
+            del x
+        print(json.dumps({"what": what, "times_s": ts, "cw_per_s_last3": B / (sum(ts[2:]) / 3)}), flush=True)
     for threads in (1, 4, 8, 12, 16, 24, 32):
         for chunk in (0, 2048, 16384):
             _abi.check(dec.lib.ldpc_decode_bits_host(dec._h, llr.ctypes.data, B, ctypes.byref(p), out.ctypes.data,

@@ -188,9 +188,11 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
     return used;
 }
 
-/* tanh sum-product, fp64: the reference module after .double() */
-static void sp_f64_one(const graph_t* g, const double* llr, int iters, double clamp, double* x, double* v2c,
-                       double* p1_out, double* z_out, uint8_t* bits_out, const wts_t* w) {
+/* tanh sum-product, fp64: the reference module after .double() (pmax = PMAX_F64).  oracle_sp_f64_pmax passes
+ * the fp32 module's bound (float)(1-1e-7) instead: fp64 arithmetic with the fp32 module's p-clamp ceiling
+ * log(16777215), the target of the fp32 kernels' soft outputs when a caller's clamp exceeds 16.6355. */
+static void sp_f64_one(const graph_t* g, const double* llr, int iters, double clamp, double pmax, double* x,
+                       double* v2c, double* p1_out, double* z_out, uint8_t* bits_out, const wts_t* w) {
     const int E = g->E;
     for (int e = 0; e < E; ++e) x[e] = 0.0;
     for (int it = 0; it < iters; ++it) {
@@ -212,8 +214,8 @@ static void sp_f64_one(const graph_t* g, const double* llr, int iters, double cl
                 double p = 1.0;
                 for (int u = a; u < b; ++u)
                     if (u != e) p *= v2c[u];
-                if (p > PMAX_F64) p = PMAX_F64;
-                if (p < -PMAX_F64) p = -PMAX_F64;
+                if (p > pmax) p = pmax;
+                if (p < -pmax) p = -pmax;
                 double y = log((1.0 + p) / (1.0 - p));
                 if (y > clamp) y = clamp;
                 if (y < -clamp) y = -clamp;
@@ -402,8 +404,8 @@ int oracle_sp_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clam
     return 0;
 }
 
-int oracle_sp_f64(GRAPH_ARGS, const double* llr, int64_t B, int iters, double clamp, double* p1, double* z,
-                  uint8_t* bits, WEIGHT_ARGS) {
+int oracle_sp_f64_pmax(GRAPH_ARGS, const double* llr, int64_t B, int iters, double clamp, double pmax, double* p1,
+                       double* z, uint8_t* bits, WEIGHT_ARGS) {
     MAKE_GRAPH;
     wts_t wt;
     const wts_t* w = make_wts(&g, &wt, w_vn, w_lw, w_fin, w_flw);
@@ -413,13 +415,19 @@ int oracle_sp_f64(GRAPH_ARGS, const double* llr, int64_t B, int iters, double cl
         double* v2c = (double*)malloc(sizeof(double) * (size_t)E);
 #pragma omp for schedule(dynamic, 16)
         for (int64_t i = 0; i < B; ++i)
-            sp_f64_one(&g, llr + i * n, iters, clamp, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
+            sp_f64_one(&g, llr + i * n, iters, clamp, pmax, x, v2c, p1 ? p1 + i * n : NULL, z ? z + i * n : NULL,
                        bits ? bits + i * n : NULL, w);
         free(x);
         free(v2c);
     }
     if (w) free((void*)wt.wofs);
     return 0;
+}
+
+int oracle_sp_f64(GRAPH_ARGS, const double* llr, int64_t B, int iters, double clamp, double* p1, double* z,
+                  uint8_t* bits, WEIGHT_ARGS) {
+    return oracle_sp_f64_pmax(m, n, E, row_ptr, col_idx, var_ptr, var_edges, llr, B, iters, clamp, PMAX_F64, p1, z,
+                              bits, w_vn, w_lw, w_fin, w_flw);
 }
 
 int oracle_ms_f32(GRAPH_ARGS, const float* llr, int64_t B, int iters, float clamp, float alpha, float beta,

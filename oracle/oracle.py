@@ -39,11 +39,13 @@ def lib():
         L.oracle_sp_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, vp, vp, vp, vp,
                                            ctypes.c_int, vp] + [vp] * 4 + [ctypes.c_int]
         L.oracle_sp_f64.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, vp, vp, vp] + [vp] * 4
+        L.oracle_sp_f64_pmax.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                                vp, vp, vp] + [vp] * 4
         L.oracle_ms_f32.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_float,
                                            ctypes.c_float, ctypes.c_int, vp, vp, vp, vp]
         L.oracle_qms.argtypes = garg + [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_int, vp, vp, vp]
-        for f in (L.oracle_sp_f32, L.oracle_sp_f64, L.oracle_ms_f32, L.oracle_qms):
+        for f in (L.oracle_sp_f32, L.oracle_sp_f64, L.oracle_sp_f64_pmax, L.oracle_ms_f32, L.oracle_qms):
             f.restype = ctypes.c_int
         L.oracle_num_threads.restype = ctypes.c_int
         _lib = L
@@ -94,7 +96,10 @@ def sp_f32(H, llr, iters, clamp, trace=False, early_stop=False, weights=None, st
     return out
 
 
-def sp_f64(H, llr, iters, clamp, weights=None):
+def sp_f64(H, llr, iters, clamp, weights=None, ceiling="f64"):
+    """tanh sum-product in fp64.  ceiling="f64": the reference's .double() module (p clamped to 1-1e-7, messages
+    <= log(19999999) = 16.8112); ceiling="f32": the same fp64 arithmetic with the fp32 module's bound
+    (float)(1-1e-7) (messages <= log(16777215) = 16.6355, bp_cv.py:44-47 as torch evaluates it in fp32)."""
     g = _graph(H)
     wp, _keep = _weights(weights, np.float64)
     llr = np.ascontiguousarray(llr, dtype=np.float64)
@@ -102,7 +107,9 @@ def sp_f64(H, llr, iters, clamp, weights=None):
     p1 = np.empty((B, g.n), np.float64)
     z = np.empty((B, g.n), np.float64)
     bits = np.empty((B, g.n), np.uint8)
-    lib().oracle_sp_f64(*_gargs(g), _ptr(llr), B, int(iters), float(clamp), _ptr(p1), _ptr(z), _ptr(bits), *wp)
+    pmax = {"f64": 1.0 - 1e-7, "f32": float(np.float32(1.0 - 1e-7))}[ceiling]
+    lib().oracle_sp_f64_pmax(*_gargs(g), _ptr(llr), B, int(iters), float(clamp), pmax, _ptr(p1), _ptr(z), _ptr(bits),
+                             *wp)
     return dict(p1=p1, z=z, bits=bits)
 
 

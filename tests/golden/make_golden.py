@@ -24,8 +24,12 @@ What it records (all .npz, numeric arrays only — loadable with allow_pickle=Fa
   * bp_x0.npz              the forward with non-zero initial messages x (bp/bp.py:43-47).
   * bp_weighted_peg64.npz  weighted BP: the reference module with random per-layer ``input_weight`` /
                            ``llr_weight`` set in memory (``bp_vc.py:19,24``), 5 iterations, fp32 and fp64.
+  * bp_<code>_sp.npz       802.11n (648,1/2), (1296,2/3), (1944,5/6): p1 and z, 5 iterations, clamp 10.
+  * bp_<code>_sp_it<k>.npz the same at 50 / 20 / 10 iterations (one reference layer looped, checked bitwise
+                           against BeliefPropagation(H, 5) first).
+  * bp_wifi648_12_sp_it50_cl20.npz  (648,1/2) 50 iterations at clamp 20, above the p-clamp ceiling.
 
-    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0]     (no argument: all)
+    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp]   (no argument: all)
 """
 import os
 import sys
@@ -267,6 +271,10 @@ def gen_wifi_sp():
 # point, iterations, reference chunk).  Memory: the reference's CV forms two (chunk, E, E) temporaries.
 WIFI_SP_LONG = [("wifi648_12", (1.0, 2.0, 3.0), 64, 50, 32), ("wifi1296_23", (2.0, 2.5, 3.0), 32, 20, 16),
                 ("wifi1944_56", (3.5, 4.0, 4.5), 16, 10, 8)]
+# the callers' other clamps (evaluate_quantized.py:20 uses 20, evaluate_snr.py:20 uses 100): messages reach the
+# reference's p-clamp ceiling log(16777215) = 16.6355 (bp_cv.py:44-47) instead of the caller's clamp
+# (any clamp >= 16.64 gives the same bits: clamp 100 was run once and its file was byte-identical to this one's)
+WIFI_SP_CLAMPS = [("wifi648_12", (2.0, 3.0), 64, 50, 32, 20.0)]
 
 
 def run_ref_looped(model, iters, clamp, llr32, double=False):
@@ -287,12 +295,13 @@ def run_ref_looped(model, iters, clamp, llr32, double=False):
     return p1.numpy(), z.numpy()
 
 
-def gen_wifi_sp_long():
+def gen_wifi_sp_long(specs=None, clamp_tag=False):
     """bp_<code>_sp_it<iters>.npz: reference tanh-SP p1 and z (fp32 module and .double()) at 50 / 20 / 10
     iterations, clamp 10, run by looping one reference layer (run_ref_looped), whose equality with the full
     BeliefPropagation(H, 5) forward is checked bitwise here first."""
     from ldpc_amd.codes import get_code
     clamp = 10.0
+    specs = specs or [(*sp, 10.0) for sp in WIFI_SP_LONG]
     H0 = np.asarray(get_code("wifi648_12")[0], dtype=np.int64)
     rng = np.random.default_rng(5050)
     enc0 = Encoder(H0)
@@ -305,7 +314,7 @@ def gen_wifi_sp_long():
         pb, zb = run_ref_looped(mm, 5, clamp, llr0, double=dbl)
         assert np.array_equal(pa, pb) and np.array_equal(za, zb), "looped layer != BeliefPropagation(H, 5)"
     print("looped reference layer == BeliefPropagation(H, 5), fp32 and fp64, bitwise", flush=True)
-    for name, snrs, B, iters, chunk in WIFI_SP_LONG:
+    for name, snrs, B, iters, chunk, clamp in specs:
         H, qc = get_code(name)
         H = np.asarray(H, dtype=np.int64)
         enc = Encoder(H)
@@ -334,7 +343,8 @@ def gen_wifi_sp_long():
             print(name, iters, tag, "bit errors:", int((np.round(p32) != cw).sum()),
                   "f32/f64 bit mismatches:", int((np.round(p32) != np.round(p64)).sum()),
                   "|dz| max", float(np.abs(z32 - z64).max()), flush=True)
-        np.savez_compressed(os.path.join(HERE, f"bp_{name}_sp_it{iters}.npz"), base=qc.base, Z=qc.Z, iters=iters,
+        fname = f"bp_{name}_sp_it{iters}" + (f"_cl{int(clamp)}" if clamp_tag else "") + ".npz"
+        np.savez_compressed(os.path.join(HERE, fname), base=qc.base, Z=qc.Z, iters=iters,
                             clamp=clamp, snrs=np.array(snrs), chunk=chunk, **rec)
 
 
@@ -368,8 +378,9 @@ def gen_x0():
 
 
 if __name__ == "__main__":
-    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong"]
+    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong", "wificlamp"]
     for part in parts:
         {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp, "x0": gen_x0,
-         "wifilong": gen_wifi_sp_long}[part]()
+         "wifilong": gen_wifi_sp_long,
+         "wificlamp": lambda: gen_wifi_sp_long(WIFI_SP_CLAMPS, clamp_tag=True)}[part]()
     print("done")

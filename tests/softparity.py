@@ -15,6 +15,12 @@ error in the log).  So the target is the reference's fp64 output, and the rules 
     or within the reference's own fp32 error on the failing codewords of the same set, whichever is larger;
     the entries where the reference's fp32 meets 1e-5 and ours does not are counted and logged.
 
+A caller's clamp above the fp32 module's p-clamp ceiling log(16777215) = 16.6355 (bp_cv.py:44-47 with the bound
+1-1e-7 rounded to fp32) lets messages reach that ceiling, which the .double() module puts at log(19999999) =
+16.8112 instead: the fp32 and fp64 modules then compute different functions.  The decoder is an fp32 drop-in, so
+for such files the z target is `z_target`: the reference's operations in fp64 with the fp32 module's bound
+(oracle sp_f64(ceiling="f32"), equal to the .double() module wherever no message reaches either ceiling).
+
 Each check appends its measured maxima to $LDPC_PARITY_LOG (JSON lines) when that is set; the GPU
 scripts collect them into profiles/.
 """
@@ -24,6 +30,16 @@ import os
 import numpy as np
 
 TOL = 1e-5
+CEILING_F32 = float(np.log(np.float64(16777215.0)))  # log((1+p)/(1-p)) at p = (float)(1-1e-7)
+
+
+def z_target(d, tag, H):
+    """The fp64 z target of golden file `d` at Eb/N0 tag `tag` (see the module docstring)."""
+    clamp = float(d["clamp"])
+    if clamp <= CEILING_F32:
+        return d[f"z_f64_{tag}"]
+    import oracle
+    return oracle.sp_f64(H, d[f"llr_{tag}"].astype(np.float64), int(d["iters"]), clamp, ceiling="f32")["z"]
 
 
 def _log(rec):

@@ -133,11 +133,11 @@ def test_oracle_wifi_codes_match_reference(path):
     (D, S) form — the GPU kernels' specification — gives the same bits and satisfies the soft-parity rule
     (tests/softparity.py) that the GPU tests apply."""
     from ldpc_amd.codes import qc_expand
-    from softparity import check_p1, check_z
+    from softparity import check_p1, check_z, z_target
     d = np.load(path)
     H = qc_expand(d["base"], int(d["Z"]))
     iters, clamp = int(d["iters"]), float(d["clamp"])
-    assert len(WIFI_SP_FILES) == 6
+    assert len(WIFI_SP_FILES) == 7
     for snr in d["snrs"]:
         tag = f"snr{snr:g}".replace(".", "p")
         llr = d[f"llr_{tag}"]
@@ -153,7 +153,29 @@ def test_oracle_wifi_codes_match_reference(path):
         assert np.array_equal(rs["bits"], ref_bits)
         label = f"oracle-ds {os.path.basename(path)[3:-4]} {tag}"
         check_p1(label, rs["p1"], d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"], H)
-        check_z(label, rs["z"], d[f"z_f32_{tag}"], d[f"z_f64_{tag}"], H)
+        check_z(label, rs["z"], d[f"z_f32_{tag}"], z_target(d, tag, H), H)
+
+
+def test_ceiling_golden_separates_f32_and_f64_modules():
+    """bp_wifi648_12_sp_it50_cl20.npz (clamp 20 > the fp32 ceiling 16.6355): the reference's fp32 and fp64 modules
+    differ there by the p-clamp ceiling alone — the oracle's fp64 with the fp64 bound follows .double(); with the
+    fp32 bound its z is >= 0.1 away from .double() on ceiling-bound entries and within the reference fp32's own
+    near-ceiling quantization of the fp32 module; the (D, S) form follows it to 1e-6 on decoded codewords."""
+    from ldpc_amd.codes import qc_expand
+    from softparity import CEILING_F32, decoded_rows
+    d = np.load(os.path.join(GOLDEN, "bp_wifi648_12_sp_it50_cl20.npz"))
+    H = qc_expand(d["base"], int(d["Z"]))
+    assert float(d["clamp"]) == 20.0 > CEILING_F32
+    llr = d["llr_snr3"]
+    t32 = oracle.sp_f64(H, llr.astype(np.float64), 50, 20.0, ceiling="f32")["z"]
+    t64 = oracle.sp_f64(H, llr.astype(np.float64), 50, 20.0)["z"]
+    assert np.abs(t64 - d["z_f64_snr3"]).max() <= 1e-8 * np.abs(t64).max()
+    assert np.abs(t32 - t64).max() > 0.1                     # the two modules' functions differ
+    conv = decoded_rows(H, t32)
+    assert conv.all()
+    rs = oracle.sp_f32(H, llr, 50, 20.0, stable=True)["z"]
+    assert (np.abs(rs - t32) / np.maximum(1.0, np.abs(t32))).max() <= 1e-6
+    assert (np.abs(d["z_f32_snr3"] - t32) / np.maximum(1.0, np.abs(t32))).max() > 1e-3  # the fp32 module's own
 
 
 def test_looped_reference_golden_settings():

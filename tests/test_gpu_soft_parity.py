@@ -8,7 +8,7 @@ Goldens were produced by the reference itself (tests/golden/make_golden.py):
 * bp_<802.11n code>_sp_it<k>.npz: the same at the iteration counts the drop-in and the BASELINE configs run —
   (648,1/2) 50 iterations x 192 codewords, (1296,2/3) 20 x 96, (1944,5/6) 10 x 48, clamp 10;
 * bp_wifi648_12_sp_it50_cl20.npz: (648,1/2) 50 iterations, clamp 20 — above the p-clamp ceiling, where the z target
-  is the fp32 module's function in fp64 (softparity.z_target).
+  is the fp32 module's function in fp64 (softparity.f64_target).
 Both kernel families run every file: the register/sliced QC kernels ("auto") and the generic CSR kernels.
 Hard decisions must equal the reference's fp32 hard decisions exactly.
 """
@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN
-from softparity import check_p1, check_z, z_target
+from softparity import check_p1, check_z, f64_target
 
 pytestmark = pytest.mark.gpu
 
@@ -65,8 +65,9 @@ def test_wifi_p1_and_z_vs_reference_f64(path, path_kind):
         assert np.array_equal(rp["bits"].cpu().numpy(), ref_bits)
         assert np.array_equal(rz["bits"].cpu().numpy(), ref_bits)
         label = f"{name} {tag} {path_kind}"
-        check_p1(label, rp["soft"].cpu().numpy(), d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"], H)
-        check_z(label, rz["soft"].cpu().numpy(), d[f"z_f32_{tag}"], z_target(d, tag, H), H)
+        p1_t, z_t = f64_target(d, tag, H)
+        check_p1(label, rp["soft"].cpu().numpy(), d[f"p1_f32_{tag}"], p1_t, H)
+        check_z(label, rz["soft"].cpu().numpy(), d[f"z_f32_{tag}"], z_t, H)
 
 
 @pytest.mark.parametrize("path", WIFI_FILES, ids=_name)

@@ -133,7 +133,7 @@ def test_oracle_wifi_codes_match_reference(path):
     (D, S) form — the GPU kernels' specification — gives the same bits and satisfies the soft-parity rule
     (tests/softparity.py) that the GPU tests apply."""
     from ldpc_amd.codes import qc_expand
-    from softparity import check_p1, check_z, z_target
+    from softparity import check_p1, check_z, f64_target
     d = np.load(path)
     H = qc_expand(d["base"], int(d["Z"]))
     iters, clamp = int(d["iters"]), float(d["clamp"])
@@ -152,8 +152,9 @@ def test_oracle_wifi_codes_match_reference(path):
         rs = oracle.sp_f32(H, llr, iters, clamp, stable=True)
         assert np.array_equal(rs["bits"], ref_bits)
         label = f"oracle-ds {os.path.basename(path)[3:-4]} {tag}"
-        check_p1(label, rs["p1"], d[f"p1_f32_{tag}"], d[f"p1_f64_{tag}"], H)
-        check_z(label, rs["z"], d[f"z_f32_{tag}"], z_target(d, tag, H), H)
+        p1_t, z_t = f64_target(d, tag, H)
+        check_p1(label, rs["p1"], d[f"p1_f32_{tag}"], p1_t, H)
+        check_z(label, rs["z"], d[f"z_f32_{tag}"], z_t, H)
 
 
 def test_ceiling_golden_separates_f32_and_f64_modules():

@@ -113,17 +113,35 @@ __device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
 // (D, S) ~ (P+ - P-, P+ + P-) with P+- = prod(1 +- a); the identity is (0, 1), one edge adds D' = D + a*S,
 // S' = S + a*D (two fma), two sets join as D = Dp*Sq + Sp*Dq, S = Sp*Sq + Dp*Dq (products, then one add —
 // symmetric, so an edge with s = +-0, a = 1, keeps D == S exactly).  The check output of an edge is
-// log(S/D) of the set of the others (= log((1+|p|)/(1-|p|))), S/D clamped to [1, RMAX] where RMAX =
-// (1+pmax)/(1-pmax) = 16777215 is the reference's fp32 p clamp (bp_cv.py:44-47) exactly, then to the
+// log(S/D) of the set of the others (= log((1+|p|)/(1-|p|))), at most log RMAX where RMAX =
+// (1+pmax)/(1-pmax) = 16777215 is the reference's fp32 p clamp (bp_cv.py:44-47) exactly, and at most the
 // caller's clamp (bp.py:47); its sign the xor of the others' signs.
+//
+// Messages travel in LOG2 UNITS ("bits"): the fp32 tanh-SP kernels' c2v messages and VC sums are the
+// natural-log values times log2(e); L stays -llr.  The VC argument is s2 = fma(L, log2 e, sum2) (one fma, as the
+// add it replaces); a = exp2(-|s2|) is one v_exp_f32 with a -|x| source modifier; the check output is
+// log2(S/D) — one v_log_f32 — clamped once to [0, cmax2], cmax2 = min(fp32(clamp * log2 e), 24 = fp32(log2
+// RMAX)); z = fma(sum2, ln2 / 2, 0.5 * L), exactly 0.5 * L when no message reaches the variable (zero
+// iterations).  Natural-log messages cost a multiply on each side (by log2 e before exp2, by ln 2 after log2)
+// and a second clamp; the results differ by rounding only (tests/softparity.py holds both to the reference's
+// fp64).
 constexpr float kRmaxF32 = 16777215.0f;
+constexpr float kLog2eF32 = 0x1.715476p+0f;    // fp32(log2 e)
+constexpr float kHalfLn2F32 = 0x1.62e430p-2f;  // fp32(ln 2 / 2): z = 0.5 * L-sum in natural units
+constexpr float kCeilLog2F32 = 24.0f;          // fp32(log2 16777215)
+__device__ __forceinline__ float sp_cmax2(float clamp) { return fminf(clamp * kLog2eF32, kCeilLog2F32); }
+// z = 0.5 * (L + sum) with the sum in log2 units (fp32) or natural units (fp64, the reference's operations)
+template <typename T> __device__ __forceinline__ T sp_z(T L, T sum) { return T(0.5) * (L + sum); }
+template <> __device__ __forceinline__ float sp_z<float>(float L, float sum2) {
+    return __builtin_fmaf(sum2, kHalfLn2F32, 0.5f * L);
+}
+// the VC argument s2 = (L + sum) * log2 e with the sum already in log2 units
+__device__ __forceinline__ float sp_vn_arg(float L, float sum2) { return __builtin_fmaf(L, kLog2eF32, sum2); }
 
-// exp(-|x|) as one v_exp_f32 of the rounded product -|x| * log2(e), with the sign of x.  The oracle's (D, S)
-// form computes the same expression (exp2f of the same fp32 product); the split-log2(e) product of the device
-// library's expf (tanh_f32 above) is not needed here: a relative error of |x| * 2^-24 in a moves the check
-// output log(S/D) by at most that much absolutely, and |x| beyond the clamp leaves it saturated.
-__device__ __forceinline__ float vn_signed_a(float x) {
-    return __builtin_copysignf(__builtin_amdgcn_exp2f(fabsf(x) * -0x1.715476p+0f), x);
+// signed a = copysign(exp(-|s|), s) of a VC sum s2 = s * log2 e: one v_exp_f32 of -|s2|.  A relative error of
+// ulp(s2) in s2 moves the check output log(S/D) by at most that much absolutely; |s| beyond the clamp saturates.
+__device__ __forceinline__ float vn_signed_a(float x2) {
+    return __builtin_copysignf(__builtin_amdgcn_exp2f(-fabsf(x2)), x2);
 }
 
 struct DSet {
@@ -133,37 +151,39 @@ __device__ __forceinline__ DSet ds_identity() { return {0.0f, 1.0f}; }
 __device__ __forceinline__ DSet ds_push(DSet x, float a) {  // a = |signed a| of one more edge
     return {__builtin_fmaf(a, x.S, x.D), __builtin_fmaf(a, x.D, x.S)};
 }
-// log(S/D) of a set, clamped, with the given sign bit (bit 31 of sgn)
-__device__ __forceinline__ float ds_out(float D, float S, uint32_t sgn, float clamp) {
-    float r = S * __builtin_amdgcn_rcpf(D);                    // D == 0: +inf -> RMAX
-    r = __builtin_amdgcn_fmed3f(r, 1.0f, kRmaxF32);
-    const float y = fminf(__builtin_amdgcn_logf(r) * 0x1.62e430p-1f, clamp);  // ln r = log2(r) * ln 2 (fp32 product)
+// log2(S/D) of a set clamped to [0, cmax2] (S >= D; a rounding below 1 gives 0; D == 0: +inf -> cmax2), with
+// the given sign bit (bit 31 of sgn)
+__device__ __forceinline__ float ds_out(float D, float S, uint32_t sgn, float cmax2) {
+    const float r = S * __builtin_amdgcn_rcpf(D);
+    const float y = __builtin_amdgcn_fmed3f(__builtin_amdgcn_logf(r), 0.0f, cmax2);
     return u2f(f2u(y) | (sgn & 0x80000000u));
 }
 // the output of an edge from its prefix set p and suffix set q (the join, then ds_out)
-__device__ __forceinline__ float ds_join_out(DSet p, DSet q, uint32_t sgn, float clamp) {
+__device__ __forceinline__ float ds_join_out(DSet p, DSet q, uint32_t sgn, float cmax2) {
     const float D = p.D * q.S + p.S * q.D;  // -ffp-contract=off: two products and one add each
     const float S = p.S * q.S + p.D * q.D;
-    return ds_out(D, S, sgn, clamp);
+    return ds_out(D, S, sgn, cmax2);
 }
 
 // One check row of compile-time degree d: g[] holds the gathered signed a of its edges (check frame) and
 // receives their outputs.  Suffix sets are built right to left, then a left-to-right pass joins each
 // edge's prefix with the suffix after it (edges 0 and d-1 need no join): 2(d-1) + 2(d-1) fma + 4(d-2)
-// products/adds.  SERIAL ties each edge's output to the running prefix (an empty asm), so the scheduler
-// keeps one edge's log in flight instead of interleaving the row's.
+// products/adds.  SERIAL = k > 0 ties every k-th edge's output to the running prefix (an empty asm), so the
+// scheduler keeps at most k edges' logs in flight instead of interleaving the whole row's (0: no ties).
 #ifndef DS_SPLIT_D
 #define DS_SPLIT_D 12  // rows longer than this run in blocks (register budget of the sliced Z = 81 kernel)
 #endif
 #ifndef DS_BLOCK
 #define DS_BLOCK 7  // (1944,5/6) d = 20: 3 blocks, 128 VGPRs spill-free at 4 waves/SIMD (10: 3 VGPRs spilled)
 #endif
-template <int d, bool SERIAL>
-__device__ __forceinline__ void cn_ds_row(float (&g)[d], float clamp) {
+template <int d, int SERIAL>
+__device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
+    const float clamp = cmax2;  // (log2 units, sp_cmax2)
+    constexpr auto tie_after = [](int t) { return SERIAL > 0 && (t + 1) % SERIAL == 0; };
     uint32_t sg = 0;
     static_for<0, d>([&](auto tt) __attribute__((always_inline)) { sg ^= f2u(g[decltype(tt)::value]); });
     if constexpr (d == 1) {
-        g[0] = ds_out(0.0f, 1.0f, 0u, clamp);  // empty product: p = 1 -> the p clamp, positive
+        g[0] = ds_out(0.0f, 1.0f, 0u, clamp);  // empty product: p = 1 -> the ceiling, positive
     } else if constexpr (d > DS_SPLIT_D) {
         // Long rows (802.11n 1944 5/6: d = 20) in blocks of DS_BLOCK edges, so only one block's suffix sets
         // are live: per block, the set T of the edges after it (fresh pushes from the row's end), then the
@@ -209,7 +229,7 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float clamp) {
                 if constexpr (t == 0) pre = {a, 1.0f};
                 else if constexpr (t < d - 1) pre = ds_push(pre, a);
                 g[t] = y;
-                if constexpr (SERIAL) asm volatile("" : "+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+                if constexpr (tie_after(t)) asm volatile("" : "+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
             });
         });
     } else {
@@ -224,14 +244,14 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float clamp) {
         });
         DSet pre = {fabsf(g[0]), 1.0f};
         g[0] = ds_out(sD[1], sS[1], sg ^ f2u(g[0]), clamp);
-        if constexpr (SERIAL) asm volatile("" : "+v"(pre.D), "+v"(g[0]));
+        if constexpr (tie_after(0)) asm volatile("" : "+v"(pre.D), "+v"(g[0]));
         static_for<1, d - 1>([&](auto tt) __attribute__((always_inline)) {
             constexpr int t = decltype(tt)::value;
             const float a = fabsf(g[t]);
             const float y = ds_join_out(pre, {sD[t + 1], sS[t + 1]}, sg ^ f2u(g[t]), clamp);
             pre = ds_push(pre, a);
             g[t] = y;
-            if constexpr (SERIAL) asm volatile("" : "+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+            if constexpr (tie_after(t)) asm volatile("" : "+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
         });
         g[d - 1] = ds_out(pre.D, pre.S, sg ^ f2u(g[d - 1]), clamp);
     }

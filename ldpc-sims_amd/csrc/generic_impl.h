@@ -31,11 +31,11 @@ namespace ldpc {
 
 constexpr int kTB = 256;
 
-// [B][n] row-major -> [n][ldb] edge-major (negated for the LLR: the reference decodes -llr, bp.py:47; as is
-// for initial c2v messages, n = E)
-template <typename T, bool NEG = true>
+// [B][n] row-major -> [n][ldb] edge-major, times `scale`: -1 for the LLR (the reference decodes -llr, bp.py:47),
+// +1 for initial c2v messages (n = E; fp32 tanh-SP: log2 e, its messages are in log2 units, common.h)
+template <typename T>
 __global__ __launch_bounds__(256) void k_load_llr(const T* __restrict__ llr, T* __restrict__ L, int64_t B, int n,
-                                                  int64_t ldb) {
+                                                  int64_t ldb, T scale) {
     __shared__ T tile[64][65];
     const int64_t cw0 = (int64_t)blockIdx.x * 64;
     const int v0 = blockIdx.y * 64;
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void k_load_llr(const T* __restrict__ llr, T* 
     for (int r = ty; r < 64; r += 4) {
         const int64_t cw = cw0 + r;
         const int v = v0 + tx;
-        if (cw < B && v < n) tile[r][tx] = NEG ? -llr[cw * n + v] : llr[cw * n + v];
+        if (cw < B && v < n) tile[r][tx] = llr[cw * n + v] * scale;
     }
     __syncthreads();
     for (int r = ty; r < 64; r += 4) {
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
                     constexpr int u = decltype(uu)::value;
                     if (u < d) S += x[u].x[i];
                 });
-                if constexpr (std::is_same_v<T, float>) o.x[i] = vn_signed_a(Lv.x[i] + S);
+                if constexpr (std::is_same_v<T, float>) o.x[i] = vn_signed_a(sp_vn_arg(Lv.x[i], S));
                 else o.x[i] = Num<T>::tanh_(T(0.5) * (Lv.x[i] + S));
                 P.x[i] += x[t].x[i];
             }
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
     });
     if constexpr (ES) {  // hard decision of APP_it = the final layer's z (bp.py:36-39,51)
 #pragma unroll
-        for (int i = 0; i < V; ++i) hb[(int64_t)v * ldb + cw + i] = (uint8_t)Num<T>::bit(T(0.5) * (Lv.x[i] + P.x[i]));
+        for (int i = 0; i < V; ++i) hb[(int64_t)v * ldb + cw + i] = (uint8_t)Num<T>::bit(sp_z<T>(Lv.x[i], P.x[i]));
     }
 }
 
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void k_vn_spw(const int32_t* __restrict__ var_
 #pragma unroll
                 for (int u = 0; u < MAXD; ++u)
                     if (u < d && u != t) S += (wv ? wv[t * d + u] : T(1)) * x[u].x[i];
-                if constexpr (std::is_same_v<T, float>) o.x[i] = vn_signed_a(lw * Lv.x[i] + S);
+                if constexpr (std::is_same_v<T, float>) o.x[i] = vn_signed_a(sp_vn_arg(lw * Lv.x[i], S));
                 else o.x[i] = Num<T>::tanh_(T(0.5) * (lw * Lv.x[i] + S));
             }
             vstore<T, V>(v2c + off[t], o);
@@ -308,6 +308,7 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
     for (int k = 0; k < MAXD; ++k) t[k] = vload<T, V>(v2c + (int64_t)(a + (k < d ? k : d - 1)) * ldb + cw);
     if constexpr (std::is_same_v<T, float>) {
         // (D, S) form: slots >= d carry a = 0, whose set is the identity, so every slot runs the same code
+        const float cmax2 = sp_cmax2(clamp);  // messages in log2 units (common.h)
         DSet suf[MAXD + 1][V];
         uint32_t sg[V];
 #pragma unroll
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
                 Vec<T, V> o;
 #pragma unroll
                 for (int i = 0; i < V; ++i) {
-                    o.x[i] = ds_join_out(pre[i], suf[e + 1][i], sg[i] ^ f2u(t[e].x[i]), clamp);
+                    o.x[i] = ds_join_out(pre[i], suf[e + 1][i], sg[i] ^ f2u(t[e].x[i]), cmax2);
                     pre[i] = ds_push(pre[i], fabsf(t[e].x[i]));
                 }
                 store_live<T, V, ES>(c2v + (int64_t)(a + e) * ldb + cw, o, done + cw);
@@ -482,7 +483,7 @@ __global__ __launch_bounds__(256) void k_final(const int32_t* __restrict__ var_p
                 T S = T(0);
                 for (int k = 0; k < d; ++k)
                     S += (fin ? fin[a + k] : T(1)) * c2v[(int64_t)var_edges[a + k] * ldb + cw];
-                z = T(0.5) * ((flw ? flw[v] : T(1)) * Lv + S);
+                z = sp_z<T>((flw ? flw[v] : T(1)) * Lv, S);  // fp32: S in log2 units
             }
             zt[vr][tx] = z;
         }
@@ -583,10 +584,11 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     const T clamp = (T)p.clamp;
     const dim3 tb(kTB);
     const unsigned gcw = (unsigned)((B + kTB - 1) / kTB);
-    k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb);
+    const T unit = (!MS && std::is_same_v<T, float>) ? T(kLog2eF32) : T(1);  // fp32 tanh-SP messages: log2 units
+    k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb, T(-1));
     // non-zero initial messages x (bp/bp.py:43-47): iteration 0 reads them like any later iteration
     const T* x0 = wts ? (const T*)wts->c2v0 : nullptr;
-    if (x0) k_load_llr<T, false><<<dim3((unsigned)((B + 63) / 64), (g.E + 63) / 64), tb, 0, st>>>(x0, c2v, B, g.E, ldb);
+    if (x0) k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.E + 63) / 64), tb, 0, st>>>(x0, c2v, B, g.E, ldb, unit);
     if (ES) {
         if (hipMemsetAsync(done, 0, (size_t)ldb, st) != hipSuccess || hipMemsetAsync(unsat, 0, (size_t)ldb, st) != hipSuccess)
             return set_error(LDPC_EHIP, "early-stop state init failed");

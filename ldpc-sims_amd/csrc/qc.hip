@@ -1012,11 +1012,24 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #ifndef QC_SP_SERIAL
 #define QC_SP_SERIAL 1
 #endif
+#ifndef QC_SP_SERIAL_STRIDE
+#define QC_SP_SERIAL_STRIDE 1  // with QC_SP_SERIAL: tie every k-th edge of a check row (k chains in flight)
+#endif
+#ifndef QC_SP_SERIAL_VN_STRIDE
+#define QC_SP_SERIAL_VN_STRIDE 1  // the same for the edges of a column
+#endif
 #ifndef QC_SP_SERIAL_ES_Z64
 #define QC_SP_SERIAL_ES_Z64 1  // serial chains in the Z > 32 early-stop kernel: spill-free (6 VGPRs spilled before), same
 #endif                         // speed ((1296,2/3) 8.42 vs 8.42 M cw/s, A/B)
 #ifndef QC_SP_WAVES_PER_SIMD_EARLY
 #define QC_SP_WAVES_PER_SIMD_EARLY 2  // 648 tanh-SP early stop 10.2 -> 12.1 M cw/s (A/B; 3 waves: 11.1)
+#endif
+// QC_SP_ADDR_MIN_USES (fixed iteration count): lane shifts used at least this many times per iteration get
+// their ds_bpermute address computed once before the loop and held in a register (as k_qc_ms_ph), instead of
+// a v_cndmask per rotation (the +4 rho folds into the ds_bpermute offset); 0 = off.  A/B (648,1/2) 50 it
+// 12.73 -> 13.10 M cw/s, (1296,2/3) 20 it 15.43-15.63 -> 15.83-15.91 (4; 5: 13.00 / 15.61; 3 spills 51 VGPRs)
+#ifndef QC_SP_ADDR_MIN_USES
+#define QC_SP_ADDR_MIN_USES 4
 #endif
 
 // Early stop (EARLY): before iteration it >= 1, the hard decisions of z_it = 0.5 * (L + ascending sum of
@@ -1057,6 +1070,20 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
             return bperm(addr, x);
         }
     };
+    // rotation addresses: "read lane (z + rho) mod Z of my group", one register per frequently used shift
+    constexpr int ADDR_MIN = EARLY ? 0 : QC_SP_ADDR_MIN_USES;
+    int ra[Z];
+    static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
+        constexpr int rho = decltype(rr)::value;
+        if constexpr (ADDR_MIN > 0 && rot_uses<C>(rho) >= ADDR_MIN)
+            ra[rho] = sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(base4, base4m) + 4 * rho;
+    });
+    (void)ra;
+    auto raddr = [&](auto rr) __attribute__((always_inline)) {
+        constexpr int rho = decltype(rr)::value;
+        if constexpr (ADDR_MIN > 0 && rot_uses<C>(rho) >= ADDR_MIN) return ra[rho];
+        else return sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(base4, base4m) + 4 * rho;
+    };
     __shared__ float Ls[(sp_tpb<EARLY>() / 64) * CPW * N];
     const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
     {
@@ -1073,6 +1100,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
+    const float cmax2 = sp_cmax2(clamp);  // check outputs in log2 units (common.h)
     constexpr uint64_t ACTIVE = lane_range_mask<Z, CPW>(0, Z);
     uint64_t done_groups = 0;  // lane masks of converged codewords (CPW == 2)
     int used_lo = iters, used_hi = iters;
@@ -1089,7 +1117,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                     });
                     int lr = lbase;
                     asm volatile("" : "+v"(lr));
-                    return 0.5f * (Ls[lr + j * Z] + S);
+                    return sp_z(Ls[lr + j * Z], S);
                 };
                 uint64_t par[MB];
 #pragma unroll
@@ -1147,10 +1175,11 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 static_for<k + 1, dj>([&](auto uu) __attribute__((always_inline)) {
                     S += msg[col_edge<C>(j, decltype(uu)::value)];
                 });
-                const float v = vn_signed_a(L + S);  // the (D, S) form's VC output (common.h)
+                const float v = vn_signed_a(sp_vn_arg(L, S));  // the (D, S) form's VC output (common.h)
                 P += msg[e];
                 msg[e] = v;
-                if constexpr (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)))
+                if constexpr (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)) &&
+                              (k + 1) % QC_SP_SERIAL_VN_STRIDE == 0)
                     asm volatile("" : "+v"(P), "+v"(msg[e]));  // next edge's sum chain starts after this output
             });
         });
@@ -1166,19 +1195,17 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 if constexpr (s == 0) {
                     g[t] = msg[e0 + t];
                 } else {
-                    const int addr = sel_lanes<wrap_mask<Z, CPW>(Z - s)>(base4, base4m) + 4 * s;
-                    g[t] = xfer(addr, msg[e0 + t]);
+                    g[t] = xfer(raddr(std::integral_constant<int, s>{}), msg[e0 + t]);
                 }
             });
-            cn_ds_row<d, (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)))>(g, clamp);
+            cn_ds_row<d, (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32))) ? QC_SP_SERIAL_STRIDE : 0>(g, cmax2);
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int s = C::SHR[r][t];
                 if constexpr (s == 0) {
                     msg[e0 + t] = g[t];
                 } else {
-                    const int addr = sel_lanes<wrap_mask<Z, CPW>(s)>(base4, base4m) + 4 * (Z - s);
-                    msg[e0 + t] = xfer(addr, g[t]);
+                    msg[e0 + t] = xfer(raddr(std::integral_constant<int, Z - s>{}), g[t]);
                 }
             });
         });
@@ -1194,7 +1221,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
             constexpr int dj = col_deg<C>(j);
             float S = 0.0f;
             static_for<0, dj>([&](auto kk) __attribute__((always_inline)) { S += msg[col_edge<C>(j, decltype(kk)::value)]; });
-            const float zz = parked ? Ls[lbase + j * Z] : 0.5f * (Ls[lbase + j * Z] + S);
+            const float zz = parked ? Ls[lbase + j * Z] : sp_z(Ls[lbase + j * Z], S);
             int t = zo + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const int64_t o = cwo * N + j * Z + t;

@@ -44,7 +44,7 @@ constexpr int nz_max() {
 // gather's positions) and the unit's waves pool one ballot per (slot, codeword) in LDS.  A codeword whose
 // syndrome is zero writes its outputs from z_it right there (iters_used = it) and is skipped at the end;
 // the unit leaves the loop when both of its codewords are done.  Bitwise equal to the generic path.
-// QC_SL_SP_SERIAL_CN: each edge's exclusive product (CN) / sum (VN) chain starts after the previous edge's
+// QC_SL_SP_SERIAL_CN = k > 0: every k-th edge's exclusive product (CN) / sum (VN) chain starts after the previous edge's
 // log / tanh output (an empty asm ties them), so one chain is in flight instead of a row's 20 partial
 // products held in registers: 195 -> 112 VGPRs for the same operations in the same order.
 // QC_SL_SP_COMPACT: one exchange buffer for v2c and c2v (a third barrier per row instead of a second
@@ -56,6 +56,9 @@ constexpr int nz_max() {
 #endif
 #ifndef QC_SL_SP_SERIAL_CN
 #define QC_SL_SP_SERIAL_CN 1
+#endif
+#ifndef QC_SL_SP_SERIAL_ROW
+#define QC_SL_SP_SERIAL_ROW QC_SL_SP_SERIAL_CN  // the check rows' ties alone (cn_ds_row's SERIAL)
 #endif
 #ifndef QC_SL_SP_COMPACT
 #define QC_SL_SP_COMPACT 1
@@ -142,6 +145,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
+    const float cmax2 = sp_cmax2(clamp);  // check outputs in log2 units (common.h)
     // outputs of this lane's codeword from z of every column (end of the loop, or at convergence)
     auto emit = [&](auto zfun) __attribute__((always_inline)) {
         if (valid) {
@@ -160,7 +164,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
         constexpr int j = decltype(jj)::value;
         float Ssum = 0.0f;
         static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) { Ssum += msg[col_edge<C>(j, decltype(kk)::value)]; });
-        return 0.5f * (Lr_at(j) + Ssum);
+        return sp_z(Lr_at(j), Ssum);
     };
     constexpr int HROW = 2 * 2 * Z;  // hard decisions: [j][half][2Z] bytes
     __shared__ uint8_t Hb[EARLY ? NB * HROW : 1];
@@ -216,7 +220,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                         static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) {
                             Ssum += msg[col_edge<C>(j, decltype(kk)::value)];
                         });
-                        Zp[(h * NB + j) * Z + zc] = 0.5f * (Lr_at(j) + Ssum);
+                        Zp[(h * NB + j) * Z + zc] = sp_z(Lr_at(j), Ssum);
                     });
                 }
                 done0 |= new0;
@@ -241,12 +245,11 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 static_for<q + 1, dj>([&](auto uu) __attribute__((always_inline)) {
                     Ssum += msg[col_edge<C>(j, decltype(uu)::value)];
                 });
-                const float v = vn_signed_a(Lj + Ssum);  // the (D, S) form's VC output (common.h)
+                const float v = vn_signed_a(sp_vn_arg(Lj, Ssum));  // the (D, S) form's VC output (common.h)
                 P += msg[e];
                 msg[e] = v;
-#if QC_SL_SP_SERIAL_CN
-                asm volatile("" : "+v"(P), "+v"(msg[e]));  // next edge's sum chain starts after this output
-#endif
+                if constexpr (QC_SL_SP_SERIAL_CN > 0 && (q + 1) % QC_SL_SP_SERIAL_CN == 0)  // k chains in flight
+                    asm volatile("" : "+v"(P), "+v"(msg[e]));  // next edge's sum chain starts after this output
             });
         });
         // CV per block row through the LDS exchange
@@ -272,7 +275,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 if constexpr (s == 0) g[t] = msg[e0 + t];
                 else g[t] = Xv[nz_index<C>(r, t) * ROW + xb + s];
             });
-            cn_ds_row<d, QC_SL_SP_SERIAL_CN != 0>(g, clamp);  // O(d) exclusive sets (common.h)
+            cn_ds_row<d, QC_SL_SP_SERIAL_ROW>(g, cmax2);  // O(d) exclusive sets (common.h)
             if constexpr (CMP) sl_barrier();  // every wave has read this row's v2c before the buffer takes its c2v
             if (live) {
                 static_for<0, d>([&](auto tt) __attribute__((always_inline)) {

@@ -77,19 +77,23 @@ static int syndrome_ok(const graph_t* g, const uint8_t* bits);
  * |p| = |prod tanh| = (S-D)/(S+D) and log((1+|p|)/(1-|p|)) = log(S/D).  Adding one edge (a, 1):
  * D' = D + a*S, S' = S + a*D; joining two sets: D = Dp*Sq + Sp*Dq, S = Sp*Sq + Dp*Dq — sums of positive
  * terms only, so every step is accurate to an ulp, where the reference's fp32 form loses digits near |p| -> 1
- * (1-p cancels; one ulp of tanh near 1 is a 1e-4..1e-3 error in log).  a = exp2(fp32(-|s| * log2 e)) and
- * ln r = fp32(log2(r) * ln 2), one transcendental each, as the GPU computes them.  Exclusive (D, S) per edge from prefix
+ * (1-p cancels; one ulp of tanh near 1 is a 1e-4..1e-3 error in log).  Exclusive (D, S) per edge from prefix
  * and suffix sets, O(d) per check.  The clamp |p| <= 1-1e-7 is S/D <= RMAX = (1+pmax)/(1-pmax) (fp32:
  * 16777215 = the reference's fp32 bound exactly), then the caller's clamp; sign = xor of the others' signs.
  * An s of +-0 gives a = 1, whose set has D == S exactly (the symmetric join keeps it so): log 1 = 0 for the
- * other edges, as the reference's p = 0. */
-#define RMAX_F32 16777215.0f  /* (1 + PMAX_F32) / (1 - PMAX_F32) in fp32 */
-static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float clamp, float* out,
+ * other edges, as the reference's p = 0.
+ * Messages in LOG2 UNITS, as the GPU kernels keep them (ldpc-sims_amd/csrc/common.h): s2 = fma(L, log2 e, sum2),
+ * a = exp2(-|s2|), the check output log2(S/D) clamped to [0, cmax2] with cmax2 = min(fp32(clamp * log2 e), 24 =
+ * fp32(log2 RMAX)), z = fma(sum2, fp32(ln 2 / 2), 0.5 * L).  The trace reports messages in natural units (x ln 2). */
+#define LOG2E_F32 1.44269502f      /* fp32(log2 e) = 0x1.715476p+0 */
+#define HALF_LN2_F32 0.346573591f  /* fp32(ln 2 / 2) = 0x1.62e430p-2 */
+#define LN2_F32 0.693147182f       /* fp32(ln 2) */
+#define CEIL_LOG2_F32 24.0f        /* fp32(log2 16777215) */
+static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float cmax2, float* out,
                           float* sufD, float* sufS) {
     if (d == 0) return;  /* an empty check (all-zero row of H) has no edges */
-    if (d == 1) {  /* empty product = 1 -> the p clamp */
-        const float y = log2f(RMAX_F32) * 0.693147182f;
-        out[0] = y > clamp ? clamp : y;
+    if (d == 1) {  /* empty product = 1 -> the p clamp: S/D = 1/0 -> the ceiling */
+        out[0] = cmax2;
         return;
     }
     uint32_t sg = 0;
@@ -107,10 +111,9 @@ static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float 
         if (t == 0) { D = sufD[1]; S = sufS[1]; }
         else if (t == d - 1) { D = pD; S = pS; }
         else { D = pD * sufS[t + 1] + pS * sufD[t + 1]; S = pS * sufS[t + 1] + pD * sufD[t + 1]; }
-        float r = S / D;                      /* D == 0 (every other a underflowed): +inf -> RMAX */
-        if (!(r <= RMAX_F32)) r = RMAX_F32;
-        float y = log2f(r) * 0.693147182f;  /* ln r as log2(r) * ln 2 in fp32, as the GPU */
-        if (y > clamp) y = clamp;
+        float y = log2f(S / D);   /* D == 0 (every other a underflowed): +inf -> the ceiling */
+        if (!(y >= 0.0f)) y = 0.0f;  /* S >= D: a ratio rounded below 1 is log 1 */
+        if (y > cmax2) y = cmax2;
         out[t] = u2f(f2u(y) | ((sg ^ f2u(sa[t])) & 0x80000000u));
         const float a = fabsf(sa[t]);
         const float nD = fmaf(a, pS, pD), nS = fmaf(a, pD, pS);
@@ -126,13 +129,15 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
                       int early_stop, uint8_t* hb, const wts_t* w, int stable, float* sufD, float* sufS) {
     const int E = g->E;
     int used = iters;
+    const float c2 = clamp * LOG2E_F32, cmax2 = c2 < CEIL_LOG2_F32 ? c2 : CEIL_LOG2_F32;
     for (int e = 0; e < E; ++e) x[e] = 0.0f;
     for (int it = 0; it < iters; ++it) {
         if (early_stop && it > 0) {
             for (int v = 0; v < g->n; ++v) {
                 float S = 0.0f;
                 for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += x[g->var_edges[u]];
-                hb[v] = (uint8_t)(0.5f * (-llr[v] + S) <= ZTHR_F32);
+                const float zv = stable ? fmaf(S, HALF_LN2_F32, 0.5f * -llr[v]) : 0.5f * (-llr[v] + S);
+                hb[v] = (uint8_t)(zv <= ZTHR_F32);
             }
             if (syndrome_ok(g, hb)) { used = it; break; }
         }
@@ -147,8 +152,8 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
                 for (int u = a; u < b; ++u)
                     if (u != t) S += wv ? wv[(t - a) * d + (u - a)] * x[g->var_edges[u]] : x[g->var_edges[u]];
                 if (stable) {  /* signed a = copysign(exp(-|s|), s), s = 2 * the reference's tanh argument */
-                    const float sv = Lw + S;
-                    v2c[g->var_edges[t]] = copysignf(exp2f(fabsf(sv) * -1.44269502f), sv);  /* fp32 product, as the GPU */
+                    const float sv = fmaf(Lw, LOG2E_F32, S);  /* log2 units */
+                    v2c[g->var_edges[t]] = copysignf(exp2f(-fabsf(sv)), sv);
                 } else {
                     v2c[g->var_edges[t]] = tanhf(0.5f * (Lw + S));
                 }
@@ -157,7 +162,7 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
         /* CV */
         for (int c = 0; c < g->m && stable; ++c) {
             const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
-            cn_stable_f32(b - a, v2c + a, clamp, x + a, sufD, sufS);
+            cn_stable_f32(b - a, v2c + a, cmax2, x + a, sufD, sufS);
         }
         for (int c = 0; c < g->m && !stable; ++c) {
             const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
@@ -173,14 +178,17 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
                 x[e] = y;
             }
         }
-        if (trace) memcpy(trace + (int64_t)it * trace_stride, x, sizeof(float) * E);
+        if (trace && stable)
+            for (int e = 0; e < E; ++e) trace[(int64_t)it * trace_stride + e] = x[e] * LN2_F32;
+        else if (trace)
+            memcpy(trace + (int64_t)it * trace_stride, x, sizeof(float) * E);
     }
     for (int v = 0; v < g->n; ++v) {
         float S = 0.0f;
         const float* fw = w && w->fin ? (const float*)w->fin : NULL;
         for (int u = g->var_ptr[v]; u < g->var_ptr[v + 1]; ++u) S += fw ? fw[u] * x[g->var_edges[u]] : x[g->var_edges[u]];
         const float Lf = w && w->flw ? ((const float*)w->flw)[v] * -llr[v] : -llr[v];
-        const float z = 0.5f * (Lf + S);
+        const float z = stable ? fmaf(S, HALF_LN2_F32, 0.5f * Lf) : 0.5f * (Lf + S);
         if (z_out) z_out[v] = z;
         if (p1_out) p1_out[v] = 1.0f - 1.0f / (1.0f + expf(-z));
         if (bits_out) bits_out[v] = (uint8_t)(z <= ZTHR_F32);

@@ -27,7 +27,7 @@ BASELINE_KERNELS = [
     r"k_cn_ms<8, (true|false), \d>",
     r"k_vn_sp<float, 8, false, \d>",
     r"k_cn_sp<float, 8, false, \d>",
-    r"k_load_llr<float, true>",
+    r"k_load_llr<float>",
     r"k_final<float, 32, (true|false)>",
     r"k_qc_sp_st<ldpc::Wifi648_12, false>",
 ]

@@ -200,9 +200,13 @@ def test_ds_form_identities():
     assert np.allclose(x, f, rtol=2e-5, atol=1e-6)
     H1 = np.array([[1]])
     r1 = oracle.sp_f32(H1, np.array([[0.5]], np.float32), 1, 100.0, trace=True, stable=True)
-    assert r1["trace"][0, 0, 0] == np.float32(np.log(np.float32(16777215.0)))
+    # messages in log2 units (ceiling fp32(log2 16777215) = 24, clamp fp32(clamp * log2 e)), traced times ln 2
+    ln2, log2e = np.float32(np.log(2.0)), np.float32(np.log2(np.e))
+    assert r1["trace"][0, 0, 0] == np.float32(24.0) * ln2
+    assert abs(float(r1["trace"][0, 0, 0]) - np.log(16777215.0)) < 2e-6
     r2 = oracle.sp_f32(H1, np.array([[0.5]], np.float32), 1, 10.0, trace=True, stable=True)
-    assert r2["trace"][0, 0, 0] == np.float32(10.0)
+    assert r2["trace"][0, 0, 0] == np.float32(np.float32(10.0) * log2e) * ln2
+    assert abs(float(r2["trace"][0, 0, 0]) - 10.0) < 2e-6
 
 
 def test_degenerate_graph_both_forms():

@@ -219,6 +219,46 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
     Vec<T, V> P;
 #pragma unroll
     for (int i = 0; i < V; ++i) P.x[i] = T(0);
+    if constexpr (std::is_same_v<T, float>) {
+        // O(d) exclusive sums in log2 units, common.h vn_excl_sums's order (suffix right to left, prefix left to
+        // right, S_t = P_t + Q_{t+1}) at this node's run-time degree d
+        float Q[MAXD][V];
+        static_for<1, MAXD>([&](auto ii) __attribute__((always_inline)) {
+            constexpr int u = MAXD - decltype(ii)::value;  // MAXD-1 .. 1
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                if (u == d - 1) Q[u][i] = x[u].x[i];
+                else if constexpr (u + 1 < MAXD) Q[u][i] = Q[u + 1][i] + x[u].x[i];  // used only when u < d - 1
+            }
+        });
+        static_for<0, MAXD>([&](auto tt) __attribute__((always_inline)) {
+            constexpr int t = decltype(tt)::value;
+            if (t < d) {
+                Vec<T, V> o;
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    float S;
+                    if constexpr (t == 0) S = d == 1 ? 0.0f : Q[1][i];
+                    else if constexpr (t + 1 < MAXD) S = t == d - 1 ? P.x[i] : P.x[i] + Q[t + 1][i];
+                    else S = P.x[i];
+                    o.x[i] = vn_signed_a(sp_vn_arg(Lv.x[i], S));
+                    P.x[i] = t == 0 ? x[0].x[i] : P.x[i] + x[t].x[i];
+                }
+                vstore<T, V>(v2c + off[t], o);
+            }
+        });
+        if constexpr (ES) {  // z of APP_it from the ascending sum 0 + x_0 + ... (the register kernels' zcol)
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                float Sa = 0.0f;
+#pragma unroll
+                for (int k = 0; k < MAXD; ++k)
+                    if (k < d) Sa += x[k].x[i];
+                hb[(int64_t)v * ldb + cw + i] = (uint8_t)Num<T>::bit(sp_z<T>(Lv.x[i], Sa));
+            }
+        }
+        return;
+    }
     // slots by static_for: x[] / off[] indices are constants (with #pragma unroll the V = 2 bodies were
     // left rolled and x[] went to scratch)
     static_for<0, MAXD>([&](auto tt) __attribute__((always_inline)) {
@@ -232,8 +272,7 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
                     constexpr int u = decltype(uu)::value;
                     if (u < d) S += x[u].x[i];
                 });
-                if constexpr (std::is_same_v<T, float>) o.x[i] = vn_signed_a(sp_vn_arg(Lv.x[i], S));
-                else o.x[i] = Num<T>::tanh_(T(0.5) * (Lv.x[i] + S));
+                o.x[i] = Num<T>::tanh_(T(0.5) * (Lv.x[i] + S));  // fp64: the reference's operations
                 P.x[i] += x[t].x[i];
             }
             vstore<T, V>(v2c + off[t], o);
@@ -246,8 +285,10 @@ __global__ __launch_bounds__(256) void k_vn_sp(const int32_t* __restrict__ var_p
 }
 
 // Weighted VC + tanh (bp_vc.py:16-27 with input_weight / llr_weight != 1): every target slot sums its own
-// weighted sources, ascending, skipping itself — the masked mm's terms in its k order.  Weights are
-// wave-uniform (scalar loads).  vn_it/lw_it point at this iteration's block (null = ones).
+// weighted sources skipping itself — fp64: ascending, the masked mm's terms in its k order; fp32: the sources
+// before it left to right plus the sources after it right to left, the association of the unweighted O(d) sums
+// (common.h vn_excl_sums), so unit weights give the unweighted messages bit for bit.  Weights are wave-uniform
+// (scalar loads).  vn_it/lw_it point at this iteration's block (null = ones).
 template <typename T, int MAXD, int V>
 __global__ __launch_bounds__(256) void k_vn_spw(const int32_t* __restrict__ var_ptr, const int32_t* __restrict__ var_edges,
                                                 const int32_t* __restrict__ wofs, const T* __restrict__ vn_it,
@@ -281,12 +322,32 @@ __global__ __launch_bounds__(256) void k_vn_spw(const int32_t* __restrict__ var_
             Vec<T, V> o;
 #pragma unroll
             for (int i = 0; i < V; ++i) {
-                T S = T(0);
+                if constexpr (std::is_same_v<T, float>) {
+                    float P = 0.0f, Q = 0.0f;
+                    bool hp = false, hq = false;
 #pragma unroll
-                for (int u = 0; u < MAXD; ++u)
-                    if (u < d && u != t) S += (wv ? wv[t * d + u] : T(1)) * x[u].x[i];
-                if constexpr (std::is_same_v<T, float>) o.x[i] = vn_signed_a(sp_vn_arg(lw * Lv.x[i], S));
-                else o.x[i] = Num<T>::tanh_(T(0.5) * (lw * Lv.x[i] + S));
+                    for (int u = MAXD - 1; u >= 0; --u)
+                        if (u < d && u > t) {
+                            const float y = (wv ? wv[t * d + u] : 1.0f) * x[u].x[i];
+                            Q = hq ? Q + y : y;
+                            hq = true;
+                        }
+#pragma unroll
+                    for (int u = 0; u < MAXD; ++u)
+                        if (u < t) {
+                            const float y = (wv ? wv[t * d + u] : 1.0f) * x[u].x[i];
+                            P = hp ? P + y : y;
+                            hp = true;
+                        }
+                    const float S = hp ? (hq ? P + Q : P) : (hq ? Q : 0.0f);
+                    o.x[i] = vn_signed_a(sp_vn_arg(lw * Lv.x[i], S));
+                } else {
+                    T S = T(0);
+#pragma unroll
+                    for (int u = 0; u < MAXD; ++u)
+                        if (u < d && u != t) S += (wv ? wv[t * d + u] : T(1)) * x[u].x[i];
+                    o.x[i] = Num<T>::tanh_(T(0.5) * (lw * Lv.x[i] + S));
+                }
             }
             vstore<T, V>(v2c + off[t], o);
         }

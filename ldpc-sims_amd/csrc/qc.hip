@@ -1086,6 +1086,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     };
     __shared__ float Ls[(sp_tpb<EARLY>() / 64) * CPW * N];
     const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
+    const int lbase4 = lbase * 4;  // bytes (lds_reload)
     {
         const int64_t cwbase = valid ? cw * N : 0;
         const float vmask = valid ? 1.0f : 0.0f;
@@ -1115,9 +1116,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                     static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) {
                         S += msg[col_edge<C>(j, decltype(kk)::value)];
                     });
-                    int lr = lbase;
-                    asm volatile("" : "+v"(lr));
-                    return sp_z(Ls[lr + j * Z], S);
+                    return sp_z(lds_reload<4 * j * Z, float>(Ls, lbase4), S);
                 };
                 uint64_t par[MB];
 #pragma unroll
@@ -1164,24 +1163,17 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             constexpr int dj = col_deg<C>(j);
-            int lr = lbase;
-            asm volatile("" : "+v"(lr));
-            const float L = Ls[lr + j * Z];
-            float P = 0.0f;
-            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
-                constexpr int k = decltype(kk)::value;
-                constexpr int e = col_edge<C>(j, k);
-                float S = P;
-                static_for<k + 1, dj>([&](auto uu) __attribute__((always_inline)) {
-                    S += msg[col_edge<C>(j, decltype(uu)::value)];
+            const float L = lds_reload<4 * j * Z, float>(Ls, lbase4);
+            constexpr bool TIE = QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32));
+            vn_excl_sums<dj, TIE ? QC_SP_SERIAL_VN_STRIDE : 0>(
+                [&](auto kk) __attribute__((always_inline)) { return msg[col_edge<C>(j, decltype(kk)::value)]; },
+                [&](auto kk, float S) __attribute__((always_inline)) {
+                    constexpr int k = decltype(kk)::value;
+                    constexpr int e = col_edge<C>(j, k);
+                    msg[e] = vn_signed_a(sp_vn_arg(L, S));  // the (D, S) form's VC output (common.h)
+                    if constexpr (TIE && (k + 1) % QC_SP_SERIAL_VN_STRIDE == 0)
+                        asm volatile("" : "+v"(msg[e]));  // next edge's chain starts after this output
                 });
-                const float v = vn_signed_a(sp_vn_arg(L, S));  // the (D, S) form's VC output (common.h)
-                P += msg[e];
-                msg[e] = v;
-                if constexpr (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32)) &&
-                              (k + 1) % QC_SP_SERIAL_VN_STRIDE == 0)
-                    asm volatile("" : "+v"(P), "+v"(msg[e]));  // next edge's sum chain starts after this output
-            });
         });
         // CV in the check frame: gather v2c, exclusive products, log, clamp, scatter c2v back
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {

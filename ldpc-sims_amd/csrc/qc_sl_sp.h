@@ -237,20 +237,15 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
             constexpr int dj = col_deg<C>(j);
             const float Lj = LPF ? Lnext : Lr_at(j);
             if constexpr (LPF && j + 1 < NB) Lnext = Lr_at(j + 1);  // in flight during this column's chains
-            float P = 0.0f;
-            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
-                constexpr int q = decltype(kk)::value;
-                constexpr int e = col_edge<C>(j, q);
-                float Ssum = P;
-                static_for<q + 1, dj>([&](auto uu) __attribute__((always_inline)) {
-                    Ssum += msg[col_edge<C>(j, decltype(uu)::value)];
+            vn_excl_sums<dj, QC_SL_SP_SERIAL_CN>(  // O(d) exclusive sums (common.h), k chains in flight
+                [&](auto kk) __attribute__((always_inline)) { return msg[col_edge<C>(j, decltype(kk)::value)]; },
+                [&](auto kk, float Ssum) __attribute__((always_inline)) {
+                    constexpr int q = decltype(kk)::value;
+                    constexpr int e = col_edge<C>(j, q);
+                    msg[e] = vn_signed_a(sp_vn_arg(Lj, Ssum));  // the (D, S) form's VC output (common.h)
+                    if constexpr (QC_SL_SP_SERIAL_CN > 0 && (q + 1) % QC_SL_SP_SERIAL_CN == 0)
+                        asm volatile("" : "+v"(msg[e]));  // next edge's chain starts after this output
                 });
-                const float v = vn_signed_a(sp_vn_arg(Lj, Ssum));  // the (D, S) form's VC output (common.h)
-                P += msg[e];
-                msg[e] = v;
-                if constexpr (QC_SL_SP_SERIAL_CN > 0 && (q + 1) % QC_SL_SP_SERIAL_CN == 0)  // k chains in flight
-                    asm volatile("" : "+v"(P), "+v"(msg[e]));  // next edge's sum chain starts after this output
-            });
         });
         // CV per block row through the LDS exchange
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {

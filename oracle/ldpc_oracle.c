@@ -147,10 +147,43 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
             const float L = -llr[v];
             const float* wv = w && w->vn ? (const float*)w->vn + it * w->W + w->wofs[v] : NULL;
             const float Lw = w && w->lw ? ((const float*)w->lw)[(int64_t)it * g->n + v] * L : L;
+            if (stable && !wv) {
+                /* exclusive sums in O(d), the GPU kernels' order: suffix Q_t = x_t + ... + x_{d-1} (right to left),
+                 * prefix P_t = x_0 + ... + x_{t-1} (left to right), S_0 = Q_1, S_{d-1} = P_{d-1}, S_t = P_t + Q_{t+1} */
+                float* Q = sufD;  /* scratch, >= d entries */
+                if (d >= 2) Q[d - 1] = x[g->var_edges[b - 1]];
+                for (int t = d - 2; t >= 1; --t) Q[t] = Q[t + 1] + x[g->var_edges[a + t]];
+                float P = 0.0f;
+                for (int t = 0; t < d; ++t) {
+                    const float xt = x[g->var_edges[a + t]];
+                    const float S = d == 1 ? 0.0f : t == 0 ? Q[1] : t == d - 1 ? P : P + Q[t + 1];
+                    P = t == 0 ? xt : P + xt;
+                    const float sv = fmaf(Lw, LOG2E_F32, S);  /* log2 units */
+                    v2c[g->var_edges[a + t]] = copysignf(exp2f(-fabsf(sv)), sv);
+                }
+                continue;
+            }
             for (int t = a; t < b; ++t) {
                 float S = 0.0f;
-                for (int u = a; u < b; ++u)
-                    if (u != t) S += wv ? wv[(t - a) * d + (u - a)] * x[g->var_edges[u]] : x[g->var_edges[u]];
+                if (stable) {  /* weighted: the O(d) association per target, sources before t left to right plus
+                                  sources after t right to left (GPU k_vn_spw) */
+                    float P = 0.0f, Q = 0.0f;
+                    int hp = 0, hq = 0;
+                    for (int u = b - 1; u > t; --u) {
+                        const float y = wv[(t - a) * d + (u - a)] * x[g->var_edges[u]];
+                        Q = hq ? Q + y : y;
+                        hq = 1;
+                    }
+                    for (int u = a; u < t; ++u) {
+                        const float y = wv[(t - a) * d + (u - a)] * x[g->var_edges[u]];
+                        P = hp ? P + y : y;
+                        hp = 1;
+                    }
+                    S = hp ? (hq ? P + Q : P) : (hq ? Q : 0.0f);
+                } else {
+                    for (int u = a; u < b; ++u)
+                        if (u != t) S += wv ? wv[(t - a) * d + (u - a)] * x[g->var_edges[u]] : x[g->var_edges[u]];
+                }
                 if (stable) {  /* signed a = copysign(exp(-|s|), s), s = 2 * the reference's tanh argument */
                     const float sv = fmaf(Lw, LOG2E_F32, S);  /* log2 units */
                     v2c[g->var_edges[t]] = copysignf(exp2f(-fabsf(sv)), sv);

@@ -626,6 +626,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     constexpr int LSTR = lstr<C>();
     __shared__ __attribute__((aligned(16))) float Ls[st_tpb<EARLY>() * LSTR];  // lane-major L rows (qc_common.h lpos)
     const int lrow = threadIdx.x * LSTR;
+    const int lrow4 = lrow * 4;  // bytes (lds_reload)
 
     constexpr bool LDSROT = EARLY ? QC_PH_LDSROT_EARLY : QC_PH_LDSROT;
     __shared__ float Rw[LDSROT ? st_tpb<EARLY>() : 1];  // one 64-lane rotation row per wave
@@ -774,9 +775,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         constexpr int j = lcol<C>(p);
         constexpr int dj = col_deg<C>(j);
         if constexpr (p % 4 == 0) {
-            int lr = lrow;
-            asm volatile("" : "+v"(lr));  // not hoisted out of the loop (register budget)
-            Lg = *static_cast<const f4*>(__builtin_assume_aligned(&Ls[lr + p], 16));
+            Lg = lds_reload<4 * p, f4, 16>(Ls, lrow4);  // not hoisted out of the loop (register budget)
         }
         float a = Lg[p % 4];
         static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
@@ -803,9 +802,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         constexpr int p = decltype(pp)::value;
         constexpr int j = lcol<C>(p);
         if constexpr (p % 4 == 0) {
-            int lr = lrow;
-            asm volatile("" : "+v"(lr));
-            Lg = *static_cast<const f4*>(__builtin_assume_aligned(&Ls[lr + p], 16));
+            Lg = lds_reload<4 * p, f4, 16>(Ls, lrow4);
         }
         float a = Lg[p % 4];
         static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) { a = a + msg[col_edge<C>(j, decltype(kk)::value)]; });
@@ -890,9 +887,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
                 if constexpr (!QC_PH_APPB_LA) back_col(pp, T[p % 2]);
                 else if constexpr (p + 1 < NB) back_col(std::integral_constant<int, p + 1>{}, T[(p + 1) % 2]);
                 if constexpr (p % 4 == 0) {
-                    int lr = lrow;
-                    asm volatile("" : "+v"(lr));
-                    Lg = *static_cast<const f4*>(__builtin_assume_aligned(&Ls[lr + p], 16));
+                    Lg = lds_reload<4 * p, f4, 16>(Ls, lrow4);
                 }
                 float a = Lg[p % 4];
                 static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) { a = a + T[p % 2][decltype(kk)::value]; });

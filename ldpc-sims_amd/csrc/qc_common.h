@@ -274,7 +274,7 @@ constexpr int rot_uses(int rho) {  // ds_bpermutes per iteration that read lane 
 // the instruction's immediate offset.  One v_mov per reload, where an opaque element index cost a v_mov and a
 // v_lshlrev (the index * 4) per reload.
 template <int OFF, class T, int ALIGN = alignof(T)>
-__device__ __forceinline__ T lds_reload(const float* base, int boff) {
+__device__ __forceinline__ T lds_reload(const void* base, int boff) {
     asm volatile("" : "+v"(boff));
     const char* p = reinterpret_cast<const char*>(base) + boff + OFF;
     return *static_cast<const T*>(__builtin_assume_aligned(p, ALIGN));

@@ -133,6 +133,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     constexpr int LSTR = lstr<C>();
     __shared__ __attribute__((aligned(16))) uint32_t Ls[pk_tpb<EARLY>() * LSTR];  // lane-major packed L rows (lpos)
     const int lrow = threadIdx.x * LSTR;
+    const int lrow4 = lrow * 4;  // bytes (lds_reload)
 
     // lane rotations through a per-wave LDS row (as k_qc_ms_ph, qc.hip QC_PH_LDSROT) or ds_bpermute
     constexpr bool LDSROT = EARLY ? QC_PK_LDSROT_EARLY : QC_PK_LDSROT;
@@ -232,9 +233,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
         constexpr int j = lcol<C>(p);
         constexpr int dj = col_deg<C>(j);
         if constexpr (p % 4 == 0) {
-            int lr = lrow;
-            asm volatile("" : "+v"(lr));  // not hoisted out of the loop (register budget)
-            Lg = *static_cast<const f4*>(__builtin_assume_aligned(&Ls[lr + p], 16));
+            Lg = lds_reload<4 * p, f4, 16>(Ls, lrow4);  // not hoisted out of the loop (register budget)
         }
         uint32_t s = __float_as_uint(Lg[p % 4]);
         static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {

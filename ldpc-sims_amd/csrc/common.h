@@ -208,6 +208,9 @@ __device__ __forceinline__ float ds_join_out(DSet p, DSet q, uint32_t sgn, float
 #ifndef DS_BLOCK
 #define DS_BLOCK 7  // (1944,5/6) d = 20: 3 blocks, 128 VGPRs spill-free at 4 waves/SIMD (10: 3 VGPRs spilled)
 #endif
+#ifndef DS_TSHARE
+#define DS_TSHARE 1
+#endif
 template <int d, int SERIAL>
 __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
     const float clamp = cmax2;  // (log2 units, sp_cmax2)
@@ -225,10 +228,31 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
         // the compiler CSEs the passes and keeps every suffix set live, which is what blocking avoids.)
         constexpr int BS = DS_BLOCK < d ? DS_BLOCK : d, NBK = (d + BS - 1) / BS;
         DSet pre = {0.0f, 1.0f};
+        // DS_TSHARE: one pass from the row's end yields every block's T (the sets at the block boundaries,
+        // the same pushes in the same order), instead of a fresh pass per block
+        [[maybe_unused]] float TD[NBK], TS[NBK];
+        if constexpr (DS_TSHARE) {
+            float a = fabsf(g[d - 1]);
+            asm volatile("" : "+v"(a));
+            DSet T = {a, 1.0f};
+            static_for<0, d - 1 - BS>([&](auto uu) __attribute__((always_inline)) {
+                constexpr int t = d - 2 - decltype(uu)::value;  // d-2 down to BS
+                float b = fabsf(g[t]);
+                asm volatile("" : "+v"(b));
+                T = ds_push(T, b);
+                if constexpr (t % BS == 0) {  // t = hi of block t / BS - 1
+                    TD[t / BS - 1] = T.D;
+                    TS[t / BS - 1] = T.S;
+                }
+            });
+        }
         static_for<0, NBK>([&](auto kk) __attribute__((always_inline)) {
             constexpr int lo = decltype(kk)::value * BS, hi = (lo + BS < d) ? lo + BS : d;
             float sD[BS + 1], sS[BS + 1];  // sD[t - lo]: set of edges t..d-1, lo < t <= hi
-            if constexpr (hi < d) {
+            if constexpr (hi < d && DS_TSHARE) {
+                sD[hi - lo] = TD[decltype(kk)::value];
+                sS[hi - lo] = TS[decltype(kk)::value];
+            } else if constexpr (hi < d) {
                 float a = fabsf(g[d - 1]);
                 asm volatile("" : "+v"(a));
                 DSet T = {a, 1.0f};

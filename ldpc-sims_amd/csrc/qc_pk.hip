@@ -87,17 +87,40 @@ constexpr int min_row_deg() {
     return m;
 }
 
-// the two smallest of D packed non-negative magnitudes (each result is one of the inputs, bit for bit)
+// three-input packed minimum (v_pk_minimum3_f16, gfx950): IEEE minimum, the same as min on these operands
+// (no NaN; magnitudes carry +0 only)
+__device__ __forceinline__ uint32_t pmin3(uint32_t a, uint32_t b, uint32_t c) {
+    return as_u(__builtin_elementwise_minimum(__builtin_elementwise_minimum(as_h2(a), as_h2(b)), as_h2(c)));
+}
+#ifndef QC_PK_MIN3
+#define QC_PK_MIN3 1  // two-minimum over edge pairs with v_pk_minimum3_f16: 5 VALU per 2 edges instead of 6
+#endif
+// the two smallest of D packed non-negative magnitudes (each result is one of the inputs, bit for bit).
+// QC_PK_MIN3, per pair (x, y) with lo/hi = min/max(x, y): the new second minimum of {mn1 <= mn2, x, y} is
+// min(mn2, hi, max(mn1, lo)) (lo < mn1: min(mn1, hi); else min(mn2, lo)), the new minimum min(mn1, lo).
 template <int D>
 __device__ __forceinline__ void two_min_pk(const uint32_t (&a)[D], uint32_t& mn1, uint32_t& mn2) {
     static_assert(D >= 2, "packed min-sum: check degree >= 2");
     mn1 = pmin(a[0], a[1]);
     mn2 = pmax(a[0], a[1]);
-    static_for<2, D>([&](auto tt) __attribute__((always_inline)) {
-        constexpr int t = decltype(tt)::value;
-        mn2 = pmin(mn2, pmax(mn1, a[t]));
-        mn1 = pmin(mn1, a[t]);
-    });
+    if constexpr (QC_PK_MIN3) {
+        static_for<0, (D - 2) / 2>([&](auto pp) __attribute__((always_inline)) {
+            constexpr int t = 2 + 2 * decltype(pp)::value;
+            const uint32_t lo = pmin(a[t], a[t + 1]), hi = pmax(a[t], a[t + 1]);
+            mn2 = pmin3(mn2, hi, pmax(mn1, lo));
+            mn1 = pmin(mn1, lo);
+        });
+        if constexpr (D % 2 == 1) {
+            mn2 = pmin(mn2, pmax(mn1, a[D - 1]));
+            mn1 = pmin(mn1, a[D - 1]);
+        }
+    } else {
+        static_for<2, D>([&](auto tt) __attribute__((always_inline)) {
+            constexpr int t = decltype(tt)::value;
+            mn2 = pmin(mn2, pmax(mn1, a[t]));
+            mn1 = pmin(mn1, a[t]);
+        });
+    }
 }
 
 template <int D>

@@ -16,14 +16,15 @@
 //   tanh-SP  k_vn_sp : v2c = tanh(0.5*(L + sum_{c'!=c} c2v))           bp_vc.py:16-27 + bp.py:29
 //            k_cn_sp : c2v = clamp(log((1+p)/(1-p)), +-clamp), p = clamp(prod_{v'!=v} v2c, +-(1-1e-7))
 //                                                                        bp_cv.py:22-50 + bp.py:47
-//            fp32 evaluates this function in the (D, S) form (common.h): the VN stores the signed
-//            a = copysign(exp(-|s|), s) instead of tanh(s/2), the CN forms each edge's exclusive set from
-//            prefix and suffix sets (O(d)) and outputs log(S/D); fp64 keeps the reference's operations.
+//            fp32 evaluates this function in the (D, S) form with messages in log2 units (common.h): the VN
+//            stores the signed a = copysign(exp2(-|s2|), s2) instead of tanh(s/2) with O(d) exclusive sums,
+//            the CN forms each edge's exclusive set from prefix and suffix sets (O(d)) and outputs
+//            log2(S/D); fp64 keeps the reference's operations.
 //   min-sum  k_vn_ms / k_cn_ms                                          (oracle/ldpc_oracle.c spec)
 //   k_final  : z = 0.5*(L + sum c2v), bits = np.round(1-sigmoid(z)), p1 = 1-sigmoid(z)   bp.py:51
 //
-// Exclusive sums/products use the prefix-then-continue form, which performs exactly the sequential
-// operations of the reference's masked reductions ("skip self, ascending order").
+// fp64 exclusive sums/products use the prefix-then-continue form, the sequential operations of the reference's
+// masked reductions ("skip self, ascending order"); fp32 tanh-SP and min-sum follow the oracle's orders.
 #pragma once
 #include "common.h"
 

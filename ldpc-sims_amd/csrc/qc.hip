@@ -991,12 +991,12 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 }
 
 // ---- tanh sum-product, register-resident (the reference's algorithm on-chip) ---------------------
-// Messages in the variable frame, one VGPR per edge (c2v between iterations, v2c inside one).  The
-// operations are the oracle's (D, S) form and the generic kernels' (bp_vc.py:16-27, bp_cv.py:22-50 evaluated
-// as in common.h): per variable, v2c_t = copysign(exp(-|L + S_t|), .) with S_t the ascending sum skipping
-// t, formed prefix-then-continue; per check (cn_ds_row), each edge's log(S/D) of the others' set, clamped
-// to the reference's p clamp and to +-clamp; final z = 0.5 * (L + ascending sum).  Same device routines, so
-// the values equal the generic GPU path's.
+// Messages in the variable frame, one VGPR per edge (c2v between iterations, v2c inside one), in log2 units.
+// The operations are the oracle's (D, S) form and the generic kernels' (bp_vc.py:16-27, bp_cv.py:22-50
+// evaluated as in common.h): per variable, v2c_t = copysign(exp2(-|fma(L, log2 e, S_t)|), .) with S_t the
+// O(d) exclusive sum (vn_excl_sums); per check (cn_ds_row), each edge's log2(S/D) of the others' set, clamped
+// to the reference's p clamp and to the caller's clamp; final z = fma(ascending sum, ln2/2, L/2).  Same device
+// routines, so the values equal the generic GPU path's bit for bit.
 #ifndef QC_SP_WAVES_PER_SIMD
 #define QC_SP_WAVES_PER_SIMD 4
 #endif

@@ -215,8 +215,13 @@ template <int d, int SERIAL>
 __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
     const float clamp = cmax2;  // (log2 units, sp_cmax2)
     constexpr auto tie_after = [](int t) { return SERIAL > 0 && (t + 1) % SERIAL == 0; };
-    uint32_t sg = 0;
-    static_for<0, d>([&](auto tt) __attribute__((always_inline)) { sg ^= f2u(g[decltype(tt)::value]); });
+    // xor of the row's sign words, three at a time (v_bitop3_b32 0x96)
+    uint32_t sg = f2u(g[0]);
+    static_for<0, (d - 1) / 2>([&](auto pp) __attribute__((always_inline)) {
+        constexpr int k = 1 + 2 * decltype(pp)::value;
+        sg = __builtin_amdgcn_bitop3_b32(sg, f2u(g[k]), f2u(g[k + 1]), 0x96);
+    });
+    if constexpr (d % 2 == 0) sg ^= f2u(g[d - 1]);
     if constexpr (d == 1) {
         g[0] = ds_out(0.0f, 1.0f, 0u, clamp);  // empty product: p = 1 -> the ceiling, positive
     } else if constexpr (d > DS_SPLIT_D) {

@@ -144,6 +144,20 @@ __device__ __forceinline__ float vn_signed_a(float x2) {
     return __builtin_copysignf(__builtin_amdgcn_exp2f(-fabsf(x2)), x2);
 }
 
+// SP_TIE(operands): the serial-chain tie of the tanh-SP kernels, an empty asm that redefines the chain's
+// values (so the next edge's chain depends on this edge's output).  Its cost: the hazard recognizer takes an
+// asm-defined VGPR for a possible transcendental result, so a VALU reading it right after gets an s_nop
+// (~100 of the (648,1/2) loop's 231).  SP_TIE_SCHED (a scheduling barrier instead, no operands) spills
+// 46 VGPRs there and 287 in the sliced kernel: not used.
+#ifndef SP_TIE_SCHED
+#define SP_TIE_SCHED 0
+#endif
+#if SP_TIE_SCHED
+#define SP_TIE(...) __builtin_amdgcn_sched_barrier(0)
+#else
+#define SP_TIE(...) asm volatile("" : __VA_ARGS__)
+#endif
+
 // VC exclusive sums of one column of compile-time degree d in O(d) — 3d - 6 adds instead of the ~d^2 / 2 of
 // re-summing the others per edge; the oracle's stable form (sp_f32_one) sums in the same order:
 // Q_k = x_k + ... + x_{d-1} right to left, P_k = x_0 + ... + x_{k-1} left to right, S_0 = Q_1,
@@ -171,7 +185,7 @@ __device__ __forceinline__ void vn_excl_sums(X&& x, Out&& out) {
             if constexpr (k == 0) P = x(kk);
             else if constexpr (k < d - 1) P = P + x(kk);
             out(kk, S);
-            if constexpr (TIE > 0 && (k + 1) % TIE == 0) asm volatile("" : "+v"(P));
+            if constexpr (TIE > 0 && (k + 1) % TIE == 0) SP_TIE("+v"(P));
         });
     }
 }
@@ -290,7 +304,7 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
                 if constexpr (t == 0) pre = {a, 1.0f};
                 else if constexpr (t < d - 1) pre = ds_push(pre, a);
                 g[t] = y;
-                if constexpr (tie_after(t)) asm volatile("" : "+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+                if constexpr (tie_after(t)) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
             });
         });
     } else {
@@ -305,14 +319,14 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
         });
         DSet pre = {fabsf(g[0]), 1.0f};
         g[0] = ds_out(sD[1], sS[1], sg ^ f2u(g[0]), clamp);
-        if constexpr (tie_after(0)) asm volatile("" : "+v"(pre.D), "+v"(g[0]));
+        if constexpr (tie_after(0)) SP_TIE("+v"(pre.D), "+v"(g[0]));
         static_for<1, d - 1>([&](auto tt) __attribute__((always_inline)) {
             constexpr int t = decltype(tt)::value;
             const float a = fabsf(g[t]);
             const float y = ds_join_out(pre, {sD[t + 1], sS[t + 1]}, sg ^ f2u(g[t]), clamp);
             pre = ds_push(pre, a);
             g[t] = y;
-            if constexpr (tie_after(t)) asm volatile("" : "+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+            if constexpr (tie_after(t)) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
         });
         g[d - 1] = ds_out(pre.D, pre.S, sg ^ f2u(g[d - 1]), clamp);
     }

@@ -1010,6 +1010,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #ifndef QC_SP_SERIAL_STRIDE
 #define QC_SP_SERIAL_STRIDE 1  // with QC_SP_SERIAL: tie every k-th edge of a check row (k chains in flight)
 #endif
+#ifndef QC_SP_VN_OUT_TIE
+#define QC_SP_VN_OUT_TIE 1  // the VC tie also pins each output (else the running sum alone: spills 50 VGPRs)
+#endif
 #ifndef QC_SP_SERIAL_VN_STRIDE
 #define QC_SP_SERIAL_VN_STRIDE 1  // the same for the edges of a column
 #endif
@@ -1166,8 +1169,8 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                     constexpr int k = decltype(kk)::value;
                     constexpr int e = col_edge<C>(j, k);
                     msg[e] = vn_signed_a(sp_vn_arg(L, S));  // the (D, S) form's VC output (common.h)
-                    if constexpr (TIE && (k + 1) % QC_SP_SERIAL_VN_STRIDE == 0)
-                        asm volatile("" : "+v"(msg[e]));  // next edge's chain starts after this output
+                    if constexpr (TIE && QC_SP_VN_OUT_TIE && (k + 1) % QC_SP_SERIAL_VN_STRIDE == 0)
+                        SP_TIE("+v"(msg[e]));  // next edge's chain starts after this output
                 });
         });
         // CV in the check frame: gather v2c, exclusive products, log, clamp, scatter c2v back

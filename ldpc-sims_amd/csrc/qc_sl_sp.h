@@ -244,7 +244,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                     constexpr int e = col_edge<C>(j, q);
                     msg[e] = vn_signed_a(sp_vn_arg(Lj, Ssum));  // the (D, S) form's VC output (common.h)
                     if constexpr (QC_SL_SP_SERIAL_CN > 0 && (q + 1) % QC_SL_SP_SERIAL_CN == 0)
-                        asm volatile("" : "+v"(msg[e]));  // next edge's chain starts after this output
+                        SP_TIE("+v"(msg[e]));  // next edge's chain starts after this output
                 });
         });
         // CV per block row through the LDS exchange

@@ -1029,6 +1029,16 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #ifndef QC_SP_ADDR_MIN_USES
 #define QC_SP_ADDR_MIN_USES 4
 #endif
+#ifndef QC_SP_LPF
+#define QC_SP_LPF 0  // VC phase: L of column j + QC_SP_LPF loaded before column j's chain (0: at its use).  A/B
+#endif               // (profiles/r03/ab/ab_sp_lpf.txt): fixed count neutral ((648,1/2) 16.10 vs 16.05-16.09 M cw/s)
+#ifndef QC_SP_LPF_EARLY
+#define QC_SP_LPF_EARLY 3  // the same in the early-stop kernel (2 waves/SIMD): (648,1/2) 27.3-27.5 -> 28.1-28.5 M cw/s
+#endif
+#ifndef QC_SP_GLA
+#define QC_SP_GLA 0  // CV phase (fixed iteration count): row r + 1's gathers issued before row r's chains; A/B
+                     // (648,1/2) 16.07 -> 15.73 M cw/s (the kernel is VALU-bound, not waiting on its gathers): off
+#endif
 
 // Early stop (EARLY): before iteration it >= 1, the hard decisions of z_it = 0.5 * (L + ascending sum of
 // c2v) — the generic VN kernel's hb, same operations — are balloted per block column and rotated into
@@ -1158,10 +1168,24 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
             }
         }
         // VC + tanh in the variable frame: c2v -> v2c in place
+        // L of column j + LPF is loaded before column j's chain (its address asm precedes the chain's ties),
+        // so its LDS latency hides under the chains instead of a lgkmcnt(0) wait per column
+        constexpr int LPF = EARLY ? QC_SP_LPF_EARLY : QC_SP_LPF;
+        float Lq[LPF > 0 ? LPF : 1];
+        static_for<0, LPF>([&](auto qq) __attribute__((always_inline)) {
+            constexpr int q = decltype(qq)::value;
+            if constexpr (q < NB) Lq[q] = lds_reload<4 * q * Z, float>(Ls, lbase4);
+        });
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             constexpr int dj = col_deg<C>(j);
-            const float L = lds_reload<4 * j * Z, float>(Ls, lbase4);
+            float L;
+            if constexpr (LPF > 0) {
+                L = Lq[j % LPF];
+                if constexpr (j + LPF < NB) Lq[j % LPF] = lds_reload<4 * (j + LPF) * Z, float>(Ls, lbase4);
+            } else {
+                L = lds_reload<4 * j * Z, float>(Ls, lbase4);
+            }
             constexpr bool TIE = QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32));
             vn_excl_sums<dj, TIE ? QC_SP_SERIAL_VN_STRIDE : 0>(
                 [&](auto kk) __attribute__((always_inline)) { return msg[col_edge<C>(j, decltype(kk)::value)]; },
@@ -1174,15 +1198,34 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 });
         });
         // CV in the check frame: gather v2c, exclusive products, log, clamp, scatter c2v back
+#if QC_SP_GLA
+        // gathers issued one row ahead, in place on msg[] (as k_qc_ms_ph's lookahead): row r + 1's rotations
+        // are in flight while row r's chains run
+        auto gather_sp = [&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                constexpr int s = C::SHR[r][t];
+                if constexpr (s != 0) msg[edge_off<C>(r) + t] = xfer(raddr(std::integral_constant<int, s>{}), msg[edge_off<C>(r) + t]);
+            });
+        };
+        if constexpr (!EARLY) gather_sp(std::integral_constant<int, 0>{});
+#endif
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
             constexpr int r = decltype(rr)::value;
             constexpr int d = C::DEG[r];
             constexpr int e0 = edge_off<C>(r);
             float g[d];
+#if QC_SP_GLA
+            constexpr bool GLA = !EARLY;
+            if constexpr (GLA && r + 1 < MB) gather_sp(std::integral_constant<int, r + 1>{});
+#else
+            constexpr bool GLA = false;
+#endif
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int s = C::SHR[r][t];
-                if constexpr (s == 0) {
+                if constexpr (s == 0 || GLA) {
                     g[t] = msg[e0 + t];
                 } else {
                     g[t] = xfer(raddr(std::integral_constant<int, s>{}), msg[e0 + t]);

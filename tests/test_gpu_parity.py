@@ -140,9 +140,10 @@ CODES = ["peg64_32", "wifi648_12", "wifi1296_23", "wifi1944_56"]
 
 
 @pytest.mark.parametrize("code", CODES)
-@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.8125, 0.0), (1.0, 0.5)])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 0.0), (0.8125, 0.0), (1.0, 0.5), (0.8125, 0.5)])
 def test_minsum_bit_exact_vs_oracle(code, alpha, beta, force_generic):
-    """min-sum is compare/add only: GPU and oracle must agree bit for bit, soft (z) included."""
+    """min-sum is compare/add only: GPU and oracle must agree bit for bit, soft (z) included.  Every
+    normalisation the kernels instantiate: plain, alpha, beta, and alpha + beta together (NORM_BOTH)."""
     H, qc = get_code(code)
     rate = 1 - H.shape[0] / H.shape[1]
     cw, llr = _llr(H, 1000, 2.0 if rate < 0.6 else 4.0, seed=11, rate=rate)

@@ -569,6 +569,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_WAVES_PER_SIMD
 #define QC_PH_WAVES_PER_SIMD 4
 #endif
+#ifndef QC_PH_ADDR_MIN_USES_EARLY
+#define QC_PH_ADDR_MIN_USES_EARLY QC_PH_ADDR_MIN_USES
+#endif
 #ifndef QC_PH_LA
 #define QC_PH_LA 1  // rotations issued this many rows / columns ahead, in place: +2.5 % (A/B 38.9 vs 38.0 M cw/s; 2: +2.0 %, 3: +1.5 %; 0: the plain phased order)
 #endif
@@ -599,6 +602,12 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_APPB_LA
 #define QC_PH_APPB_LA 1  // back-rotations of column p + 1 issued before column p's sum (0: in the column's own order)
 #endif
+#ifndef QC_PH_ES_ROWS
+#define QC_PH_ES_ROWS 1  // early stop: syndrome row by row with an early exit.  A/B (648,1/2) 50 it
+#endif                   // (profiles/r03/ab/ab_ph_esrows.txt): SQ_INSTS_SALU 495 M per launch against 864 M VALU in
+                         // the all-rows form; the row scan built with the default scheduler (qc_ph_es.hip, 13
+                         // VGPRs spilled) 62.9-66.4 -> 69.7-70.3 M cw/s; under iterative-ILP it spills 63 (with 5
+                         // address registers spill-free: 67.5-68.0)
 #ifndef QC_PH_WAVES_PER_SIMD_EARLY
 #define QC_PH_WAVES_PER_SIMD_EARLY 3  // spill-free (145 VGPRs): 648 min-sum early stop 24.6 -> 57.9 M cw/s (A/B)
 #endif
@@ -649,17 +658,18 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     };
     // rotation addresses, one register per distinct shift used often enough (the others: one v_cndmask
     // per use, as k_qc_ms_st)
+    constexpr int AMU = EARLY ? QC_PH_ADDR_MIN_USES_EARLY : QC_PH_ADDR_MIN_USES;
     int ra[Z];
     static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
         constexpr int rho = decltype(rr)::value;
-        if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES)
+        if constexpr (rot_uses<C>(rho) >= AMU)
             ra[rho] = sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho;
     });
     auto rot = [&](auto rr, float x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
         constexpr int rho = decltype(rr)::value;
         if constexpr (rho == 0) {
             return x;
-        } else if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES) {
+        } else if constexpr (rot_uses<C>(rho) >= AMU) {
             return xfer(ra[rho], x);
         } else {
             return xfer(sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho, x);
@@ -833,7 +843,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
     auto row_get = [&](auto rr) __attribute__((always_inline)) {  // lane (z + rho) mod Z of the last row_put
         constexpr int rho = decltype(rr)::value;
         int addr;
-        if constexpr (rot_uses<C>(rho) >= QC_PH_ADDR_MIN_USES) addr = ra[rho];
+        if constexpr (rot_uses<C>(rho) >= AMU) addr = ra[rho];
         else addr = sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho;
         return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(Rw) + addr);
     };
@@ -913,6 +923,32 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         if constexpr (EARLY) {
             // APP_{it+1} of every column (kept until the syndrome verdict), hard-decision ballots
             float app[NB];
+#if QC_PH_ES_ROWS
+            // Row by row with an early exit (as the packed kernel's QC_PK_ES_ROWS): `cand` starts as the lane
+            // groups (codewords) not yet done and loses each one whose row parity is nonzero; the scan stops once
+            // neither codeword of the wave can still be satisfied — at low Eb/N0 after the first row.  The
+            // ballots are taken at each use.  The decision equals the all-rows form's.
+            static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
+                constexpr int p = decltype(pp)::value;
+                app[lcol<C>(p)] = vn_col(pp);
+            });
+            uint64_t cand = (G0 | G1) & ~done_groups;
+            static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                constexpr int r = decltype(rr)::value;
+                if (cand) {
+                    uint64_t par = 0;
+                    static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                        constexpr int t = decltype(tt)::value;
+                        const uint64_t b = __ballot(app[C::COL[r][t]] <= thr2) & ACTIVE;
+                        par ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                    });
+                    par &= ACTIVE;
+                    if (par & G0) cand &= ~G0;
+                    if (par & G1) cand &= ~G1;
+                }
+            });
+            const uint64_t fresh = cand;
+#else
             uint64_t par[MB];
 #pragma unroll
             for (int r = 0; r < MB; ++r) par[r] = 0;
@@ -933,6 +969,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
             unsat &= ACTIVE;
             const uint64_t newly = ((unsat & G0) ? 0 : G0) | ((unsat & G1) ? 0 : G1);
             const uint64_t fresh = newly & ~done_groups;
+#endif
             if (fresh) {
                 // park the converged codeword's APP in its L row (L is no longer needed by it)
                 if (fresh & G0) used_lo = it + 1;
@@ -1265,6 +1302,44 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     }
 }
 
+#ifndef QC_PH_ES_TU
+#define QC_PH_ES_TU 1  // the float early-stop phased min-sum kernels come from qc_ph_es.hip (0: instantiated here)
+#endif
+#if QC_TU_PH_ES
+// qc_ph_es.hip includes this file with QC_TU_PH_ES = 1 and builds it with the default scheduler: it instantiates
+// only the float early-stop phased min-sum kernels (k_qc_ms_ph<C, false, true, N>), whose row-wise syndrome
+// (QC_PH_ES_ROWS) runs 5-6 % faster there than the all-rows form under iterative-ILP, which spills it
+template <class C>
+static int launch_ms_ph_es(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
+                           hipStream_t st) {
+    static_assert(C::Z <= 32, "phased kernel: two codewords per wave");
+    const int64_t waves = (B + 1) / 2;
+    const int tpb = st_tpb<true>();
+    const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
+    const float* x = (const float*)llr;
+    float* sf = (float*)soft;
+    const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
+#define FE(N) k_qc_ms_ph<C, false, true, N><<<blocks, tpb, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used)
+    switch (norm) {
+        case NORM_PLAIN: FE(NORM_PLAIN); break;
+        case NORM_ALPHA: FE(NORM_ALPHA); break;
+        case NORM_BETA: FE(NORM_BETA); break;
+        default: FE(NORM_BOTH);
+    }
+#undef FE
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
+    return LDPC_OK;
+}
+int qc_launch_ms_ph_es_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                                  int32_t* used, hipStream_t st) {
+    return launch_ms_ph_es<Wifi648_12>(llr, B, p, bits, soft, used, st);
+}
+#else
+// float early-stop phased min-sum (qc_ph_es.hip)
+int qc_launch_ms_ph_es_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                                  int32_t* used, hipStream_t st);
+
 // packed quantized kernels (qc_pk.hip)
 int qc_launch_qms_pk_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
                                 int32_t* used, hipStream_t st);
@@ -1322,10 +1397,13 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #undef QL
 #endif
     } else {
+        if constexpr (QC_PHASED != 0 && QC_PH_ES_TU != 0 && std::is_same_v<C, Wifi648_12>) {
+            if (es) return qc_launch_ms_ph_es_wifi648_12(llr, B, p, bits, soft, used, st);
+        }
         const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
 #define FL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if constexpr (QC_PHASED != 0 && C::Z <= 32)                                                             \
+        if constexpr (QC_PHASED != 0 && C::Z <= 32 && !(E && QC_PH_ES_TU != 0))                                \
             k_qc_ms_ph<C, false, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else if constexpr (QC_STORED != 0)                                                                        \
             k_qc_ms_st<C, false, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
@@ -1386,5 +1464,6 @@ int qc_decode(const QCSpec* s, const void* llr, int64_t B, const ldpc_params& p,
               int32_t* used, char*, hipStream_t st) {
     return s->launch_ms(llr, B, p, bits, soft, used, st);
 }
+#endif  // QC_TU_PH_ES
 
 }  // namespace ldpc

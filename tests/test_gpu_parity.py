@@ -231,14 +231,17 @@ def test_qc_kernel_is_selected(code):
 
 @pytest.mark.parametrize("code", QC_CODES)
 @pytest.mark.parametrize("snr", [1.0, 2.5, 4.0])
-def test_qc_early_stop_vs_oracle(code, snr):
+@pytest.mark.parametrize("alpha,beta", [(0.8125, 0.0), (1.0, 0.0), (1.0, 0.5), (0.8125, 0.5)])
+def test_qc_early_stop_vs_oracle(code, snr, alpha, beta):
+    """Early-stop min-sum, every normalisation (the (648,1/2) kernels come from qc_ph_es.hip): iteration counts,
+    bits and z bitwise equal to the oracle; 777 codewords leave the last wave's second codeword empty."""
     H, qc = get_code(code)
     rate = 1 - H.shape[0] / H.shape[1]
     cw, llr = _llr(H, 777, snr + (2.0 if rate > 0.6 else 0.0), seed=int(snr * 10), rate=rate)
     dec = ldpc_amd.get_decoder(H)
-    r = dec.decode(torch.from_numpy(llr).cuda(), 20, algo="minsum", clamp=20.0, alpha=0.8125, early_stop=True,
-                   soft="z", want_iters=True)
-    ref = oracle.ms_f32(H, llr, 20, 20.0, 0.8125, 0.0, early_stop=True)
+    r = dec.decode(torch.from_numpy(llr).cuda(), 20, algo="minsum", clamp=20.0, alpha=alpha, beta=beta,
+                   early_stop=True, soft="z", want_iters=True)
+    ref = oracle.ms_f32(H, llr, 20, 20.0, alpha, beta, early_stop=True)
     assert np.array_equal(r["iters_used"].cpu().numpy(), ref["iters_used"])
     assert np.array_equal(r["bits"].cpu().numpy(), ref["bits"])
     assert np.array_equal(r["soft"].cpu().numpy().view(np.uint32), ref["z"].view(np.uint32))

@@ -301,6 +301,9 @@ constexpr int sp_tpb() { return EARLY ? QC_SP_TPB_EARLY : 256; }
 #define QC_ST_WAVES_PER_SIMD 3  // dispatched for Z > 32 ((1296,2/3)): spill-free at 134 VGPRs, 41.0 vs 39.9 M cw/s at 4
                                 // waves (2-5 VGPRs spilled; A/B, 20 it)
 #endif
+#ifndef QC_ST_ES_ROWS
+#define QC_ST_ES_ROWS 0  // early stop, one codeword per wave: syndrome row by row with an early exit (A/B)
+#endif
 #ifndef QC_ST_WAVES_PER_SIMD_EARLY
 #define QC_ST_WAVES_PER_SIMD_EARLY 4  // early stop keeps APP_it and the syndrome ballots live: 14-15 VGPRs spill at
                                       // 4 waves, yet 3 waves (spill-free) measured 9 % slower on (1296,2/3)
@@ -385,10 +388,31 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
                 // syndrome of APP_it: per block column one ballot of the hard decisions (bit = APP <= 2*ZTHR;
                 // quantized: APP < 0, the same for integers), then per check row the XOR of its columns'
                 // masks rotated into the check frame by the edge's lane shift
+                const float thr2 = 2.0f * kZthrF32;
+                if constexpr (QC_ST_ES_ROWS && CPW == 1) {
+                    // row by row with an early exit (as k_qc_ms_ph's QC_PH_ES_ROWS): the codeword is still
+                    // unsatisfied once one row's parity is nonzero, usually at the first row
+                    bool sat = true;
+                    static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                        constexpr int r = decltype(rr)::value;
+                        if (sat) {
+                            uint64_t par = 0;
+                            static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                                constexpr int t = decltype(tt)::value;
+                                const uint64_t b = __ballot(app[C::COL[r][t]] <= thr2) & ACTIVE;
+                                par ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                            });
+                            if (par & ACTIVE) sat = false;
+                        }
+                    });
+                    if (sat) {  // the wave's codeword satisfies every check: APP_it is the output
+                        used_lo = it;
+                        break;
+                    }
+                } else {
                 uint64_t par[MB];
 #pragma unroll
                 for (int r = 0; r < MB; ++r) par[r] = 0;
-                const float thr2 = 2.0f * kZthrF32;
                 static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
                     constexpr int j = decltype(jj)::value;
                     const uint64_t b = __ballot(app[j] <= thr2) & ACTIVE;
@@ -426,6 +450,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
                         if (done_groups == (G0 | G1)) break;
                     }
                 }
+                }  // all rows
             }
         }
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {

@@ -302,7 +302,8 @@ constexpr int sp_tpb() { return EARLY ? QC_SP_TPB_EARLY : 256; }
                                 // waves (2-5 VGPRs spilled; A/B, 20 it)
 #endif
 #ifndef QC_ST_ES_ROWS
-#define QC_ST_ES_ROWS 0  // early stop, one codeword per wave: syndrome row by row with an early exit (A/B)
+#define QC_ST_ES_ROWS 1  // early stop, one codeword per wave: syndrome row by row with an early exit; A/B (1296,2/3)
+                         // 20 it (profiles/r03/ab/ab_st_esrows.txt): 54.4-54.9 -> 58.5-59.0 M cw/s in qc_ms_es.hip
 #endif
 #ifndef QC_ST_WAVES_PER_SIMD_EARLY
 #define QC_ST_WAVES_PER_SIMD_EARLY 4  // early stop keeps APP_it and the syndrome ballots live: 14-15 VGPRs spill at
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_ES_ROWS
 #define QC_PH_ES_ROWS 1  // early stop: syndrome row by row with an early exit.  A/B (648,1/2) 50 it
 #endif                   // (profiles/r03/ab/ab_ph_esrows.txt): SQ_INSTS_SALU 495 M per launch against 864 M VALU in
-                         // the all-rows form; the row scan built with the default scheduler (qc_ph_es.hip, 13
+                         // the all-rows form; the row scan built with the default scheduler (qc_ms_es.hip, 13
                          // VGPRs spilled) 62.9-66.4 -> 69.7-70.3 M cw/s; under iterative-ILP it spills 63 (with 5
                          // address registers spill-free: 67.5-68.0)
 #ifndef QC_PH_WAVES_PER_SIMD_EARLY
@@ -1327,24 +1328,31 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     }
 }
 
-#ifndef QC_PH_ES_TU
-#define QC_PH_ES_TU 1  // the float early-stop phased min-sum kernels come from qc_ph_es.hip (0: instantiated here)
+#ifndef QC_MS_ES_TU
+#define QC_MS_ES_TU 1  // the float early-stop min-sum kernels come from qc_ms_es.hip (0: instantiated here)
 #endif
-#if QC_TU_PH_ES
-// qc_ph_es.hip includes this file with QC_TU_PH_ES = 1 and builds it with the default scheduler: it instantiates
-// only the float early-stop phased min-sum kernels (k_qc_ms_ph<C, false, true, N>), whose row-wise syndrome
-// (QC_PH_ES_ROWS) runs 5-6 % faster there than the all-rows form under iterative-ILP, which spills it
+#if QC_TU_MS_ES
+// qc_ms_es.hip includes this file with QC_TU_MS_ES = 1 and builds it with the default scheduler: it instantiates
+// only the float early-stop min-sum kernels (k_qc_ms_ph<C, false, true, N> for Z <= 32, k_qc_ms_st<C, false,
+// true, N> above), whose row-wise syndromes (QC_PH_ES_ROWS, QC_ST_ES_ROWS) run faster there than under the
+// iterative-ILP scheduler of the fixed-count kernels (A/B profiles/r03/ab/ab_ph_esrows.txt, ab_st_esrows.txt)
 template <class C>
-static int launch_ms_ph_es(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
-                           hipStream_t st) {
-    static_assert(C::Z <= 32, "phased kernel: two codewords per wave");
-    const int64_t waves = (B + 1) / 2;
+static int launch_ms_es(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
+                        hipStream_t st) {
+    constexpr int CPW = (C::Z <= 32) ? 2 : 1;
+    const int64_t waves = (B + CPW - 1) / CPW;
     const int tpb = st_tpb<true>();
     const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
     const float* x = (const float*)llr;
     float* sf = (float*)soft;
     const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
-#define FE(N) k_qc_ms_ph<C, false, true, N><<<blocks, tpb, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used)
+#define FE(N)                                                                                                     \
+    do {                                                                                                          \
+        if constexpr (C::Z <= 32)                                                                                 \
+            k_qc_ms_ph<C, false, true, N><<<blocks, tpb, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
+        else                                                                                                      \
+            k_qc_ms_st<C, false, true, N><<<blocks, tpb, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
+    } while (0)
     switch (norm) {
         case NORM_PLAIN: FE(NORM_PLAIN); break;
         case NORM_ALPHA: FE(NORM_ALPHA); break;
@@ -1356,14 +1364,20 @@ static int launch_ms_ph_es(const void* llr, int64_t B, const ldpc_params& p, uin
     if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
     return LDPC_OK;
 }
-int qc_launch_ms_ph_es_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
-                                  int32_t* used, hipStream_t st) {
-    return launch_ms_ph_es<Wifi648_12>(llr, B, p, bits, soft, used, st);
+int qc_launch_ms_es_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                               int32_t* used, hipStream_t st) {
+    return launch_ms_es<Wifi648_12>(llr, B, p, bits, soft, used, st);
+}
+int qc_launch_ms_es_wifi1296_23(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                                int32_t* used, hipStream_t st) {
+    return launch_ms_es<Wifi1296_23>(llr, B, p, bits, soft, used, st);
 }
 #else
-// float early-stop phased min-sum (qc_ph_es.hip)
-int qc_launch_ms_ph_es_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
-                                  int32_t* used, hipStream_t st);
+// float early-stop min-sum (qc_ms_es.hip)
+int qc_launch_ms_es_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                               int32_t* used, hipStream_t st);
+int qc_launch_ms_es_wifi1296_23(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
+                                int32_t* used, hipStream_t st);
 
 // packed quantized kernels (qc_pk.hip)
 int qc_launch_qms_pk_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
@@ -1422,13 +1436,17 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #undef QL
 #endif
     } else {
-        if constexpr (QC_PHASED != 0 && QC_PH_ES_TU != 0 && std::is_same_v<C, Wifi648_12>) {
-            if (es) return qc_launch_ms_ph_es_wifi648_12(llr, B, p, bits, soft, used, st);
+        if constexpr (QC_PHASED != 0 && QC_STORED != 0 && QC_MS_ES_TU != 0) {
+            if (es) {
+                if constexpr (std::is_same_v<C, Wifi648_12>) return qc_launch_ms_es_wifi648_12(llr, B, p, bits, soft, used, st);
+                else return qc_launch_ms_es_wifi1296_23(llr, B, p, bits, soft, used, st);
+            }
         }
         const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
 #define FL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if constexpr (QC_PHASED != 0 && C::Z <= 32 && !(E && QC_PH_ES_TU != 0))                                \
+        if constexpr (E && QC_PHASED != 0 && QC_STORED != 0 && QC_MS_ES_TU != 0) {                              \
+        } else if constexpr (QC_PHASED != 0 && C::Z <= 32)                                                      \
             k_qc_ms_ph<C, false, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else if constexpr (QC_STORED != 0)                                                                        \
             k_qc_ms_st<C, false, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
@@ -1489,6 +1507,6 @@ int qc_decode(const QCSpec* s, const void* llr, int64_t B, const ldpc_params& p,
               int32_t* used, char*, hipStream_t st) {
     return s->launch_ms(llr, B, p, bits, soft, used, st);
 }
-#endif  // QC_TU_PH_ES
+#endif  // QC_TU_MS_ES
 
 }  // namespace ldpc

@@ -16,7 +16,7 @@ _RUNS = [("sp32", "float", 0, 0), ("sp32_es", "float", 0, 1), ("sp64", "double",
 SRCS = [("abi.hip", "abi.hip.o", []), ("generic.hip", "generic.hip.o", [])] + [
     ("generic_run.hip", f"generic_run_{n}.o", [f"-DRUN_T={t}", f"-DRUN_MS={ms}", f"-DRUN_ES={es}", f"-DRUN_NAME=generic_run_{n}"])
     for (n, t, ms, es) in _RUNS] + [("qc.hip", "qc.hip.o", []), ("qc_sl.hip", "qc_sl.hip.o", []), ("qc_pk.hip", "qc_pk.hip.o", []),
-           ("qc_sl_es.hip", "qc_sl_es.hip.o", []), ("qc_ms_es.hip", "qc_ms_es.hip.o", []),
+           ("qc_sl_es.hip", "qc_sl_es.hip.o", []), ("qc_es.hip", "qc_es.hip.o", []),
            ("channel.hip", "channel.hip.o", [])]
 OUT = os.path.join(HERE, "ldpc_amd", "libldpc_hip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
@@ -32,7 +32,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
 # otherwise (the loop is latency- and issue-limited at the 128-VGPR / 4-waves budget).
 SCHED = ["-mllvm", "--amdgpu-sched-strategy=iterative-ilp"]
 PER_FILE = {"qc.hip": ["-fno-honor-nans", *SCHED], "qc_sl.hip": ["-fno-honor-nans", *SCHED],
-            "qc_pk.hip": ["-fno-honor-nans"], "qc_sl_es.hip": ["-fno-honor-nans"], "qc_ms_es.hip": ["-fno-honor-nans"]}  # iterative-ilp crashes the register allocator on qc_pk (ROCm 7.2)
+            "qc_pk.hip": ["-fno-honor-nans"], "qc_sl_es.hip": ["-fno-honor-nans"], "qc_es.hip": ["-fno-honor-nans"]}  # iterative-ilp crashes the register allocator on qc_pk (ROCm 7.2)
 
 
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), per_file=True, qc_flags=None) -> str:

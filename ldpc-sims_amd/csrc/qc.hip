@@ -303,7 +303,7 @@ constexpr int sp_tpb() { return EARLY ? QC_SP_TPB_EARLY : 256; }
 #endif
 #ifndef QC_ST_ES_ROWS
 #define QC_ST_ES_ROWS 1  // early stop, one codeword per wave: syndrome row by row with an early exit; A/B (1296,2/3)
-                         // 20 it (profiles/r03/ab/ab_st_esrows.txt): 54.4-54.9 -> 58.5-59.0 M cw/s in qc_ms_es.hip
+                         // 20 it (profiles/r03/ab/ab_st_esrows.txt): 54.4-54.9 -> 58.5-59.0 M cw/s in qc_es.hip
 #endif
 #ifndef QC_ST_WAVES_PER_SIMD_EARLY
 #define QC_ST_WAVES_PER_SIMD_EARLY 4  // early stop keeps APP_it and the syndrome ballots live: 14-15 VGPRs spill at
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_ES_ROWS
 #define QC_PH_ES_ROWS 1  // early stop: syndrome row by row with an early exit.  A/B (648,1/2) 50 it
 #endif                   // (profiles/r03/ab/ab_ph_esrows.txt): SQ_INSTS_SALU 495 M per launch against 864 M VALU in
-                         // the all-rows form; the row scan built with the default scheduler (qc_ms_es.hip, 13
+                         // the all-rows form; the row scan built with the default scheduler (qc_es.hip, 13
                          // VGPRs spilled) 62.9-66.4 -> 69.7-70.3 M cw/s; under iterative-ILP it spills 63 (with 5
                          // address registers spill-free: 67.5-68.0)
 #ifndef QC_PH_WAVES_PER_SIMD_EARLY
@@ -1098,6 +1098,10 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #ifndef QC_SP_LPF_EARLY
 #define QC_SP_LPF_EARLY 3  // the same in the early-stop kernel (2 waves/SIMD): (648,1/2) 27.3-27.5 -> 28.1-28.5 M cw/s
 #endif
+#ifndef QC_SP_ES_ROWS
+#define QC_SP_ES_ROWS 1  // early stop: syndrome row by row with an early exit, built in qc_es.hip (A/B
+                         // profiles/r03/ab/ab_sp_esrows.txt: (648,1/2) 50 it 28.6 -> 29.2, (1296,2/3) 20 it 23.5 -> 24.8 M cw/s)
+#endif
 #ifndef QC_SP_GLA
 #define QC_SP_GLA 0  // CV phase (fixed iteration count): row r + 1's gathers issued before row r's chains; A/B
                      // (648,1/2) 16.07 -> 15.73 M cw/s (the kernel is VALU-bound, not waiting on its gathers): off
@@ -1189,6 +1193,34 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                     });
                     return sp_z(lds_reload<4 * j * Z, float>(Ls, lbase4), S);
                 };
+#if QC_SP_ES_ROWS
+                // row by row with an early exit (as the min-sum kernels): the columns' hard decisions packed in
+                // one register, then each row's parity from ballots of its columns' bits until no codeword of
+                // the wave can still be satisfied
+                uint32_t hd = 0;
+                static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+                    constexpr int j = decltype(jj)::value;
+                    hd |= Num<float>::bit(zcol(jj)) ? (1u << j) : 0u;
+                });
+                constexpr uint64_t GA = lane_range_mask<Z, 1>(0, Z), GB = (CPW == 2) ? (GA << 32) : 0;
+                uint64_t cand = (GA | GB) & ~done_groups;
+                static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+                    constexpr int r = decltype(rr)::value;
+                    if (cand) {
+                        uint64_t par = 0;
+                        static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
+                            constexpr int t = decltype(tt)::value;
+                            const uint64_t b = __ballot((hd >> C::COL[r][t]) & 1u) & ACTIVE;
+                            par ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                        });
+                        if (par & GA) cand &= ~GA;
+                        if constexpr (CPW == 2) {
+                            if (par & GB) cand &= ~GB;
+                        }
+                    }
+                });
+                const uint64_t unsat = (GA | GB) & ~cand;
+#else
                 uint64_t par[MB];
 #pragma unroll
                 for (int r = 0; r < MB; ++r) par[r] = 0;
@@ -1205,6 +1237,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
 #pragma unroll
                 for (int r = 0; r < MB; ++r) unsat |= par[r];
                 unsat &= ACTIVE;
+#endif
                 if constexpr (CPW == 1) {
                     if (unsat == 0) {  // the wave's codeword converged: its c2v are the output's
                         used_lo = it;
@@ -1328,13 +1361,13 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     }
 }
 
-#ifndef QC_MS_ES_TU
-#define QC_MS_ES_TU 1  // the float early-stop min-sum kernels come from qc_ms_es.hip (0: instantiated here)
+#ifndef QC_ES_TU
+#define QC_ES_TU 1  // the float early-stop min-sum and tanh-SP register kernels come from qc_es.hip (0: instantiated here)
 #endif
-#if QC_TU_MS_ES
-// qc_ms_es.hip includes this file with QC_TU_MS_ES = 1 and builds it with the default scheduler: it instantiates
-// only the float early-stop min-sum kernels (k_qc_ms_ph<C, false, true, N> for Z <= 32, k_qc_ms_st<C, false,
-// true, N> above), whose row-wise syndromes (QC_PH_ES_ROWS, QC_ST_ES_ROWS) run faster there than under the
+#if QC_TU_ES
+// qc_es.hip includes this file with QC_TU_ES = 1 and builds it with the default scheduler: it instantiates
+// only the early-stop register kernels (k_qc_ms_ph<C, false, true, N> for Z <= 32, k_qc_ms_st<C, false,
+// true, N> above, k_qc_sp_st<C, true>), whose row-wise syndromes (QC_PH/ST/SP_ES_ROWS) run faster there than under the
 // iterative-ILP scheduler of the fixed-count kernels (A/B profiles/r03/ab/ab_ph_esrows.txt, ab_st_esrows.txt)
 template <class C>
 static int launch_ms_es(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
@@ -1364,16 +1397,30 @@ static int launch_ms_es(const void* llr, int64_t B, const ldpc_params& p, uint8_
     if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
     return LDPC_OK;
 }
+template <class C>
+static int launch_sp_es(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
+                        hipStream_t st) {
+    constexpr int CPW = (C::Z <= 32) ? 2 : 1;
+    const int64_t waves = (B + CPW - 1) / CPW;
+    const int tpb = sp_tpb<true>();
+    const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
+    k_qc_sp_st<C, true><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
+    return LDPC_OK;
+}
 int qc_launch_ms_es_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
                                int32_t* used, hipStream_t st) {
-    return launch_ms_es<Wifi648_12>(llr, B, p, bits, soft, used, st);
+    return p.algo == LDPC_ALGO_TANH_SP ? launch_sp_es<Wifi648_12>(llr, B, p, bits, soft, used, st)
+                                       : launch_ms_es<Wifi648_12>(llr, B, p, bits, soft, used, st);
 }
 int qc_launch_ms_es_wifi1296_23(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
                                 int32_t* used, hipStream_t st) {
-    return launch_ms_es<Wifi1296_23>(llr, B, p, bits, soft, used, st);
+    return p.algo == LDPC_ALGO_TANH_SP ? launch_sp_es<Wifi1296_23>(llr, B, p, bits, soft, used, st)
+                                       : launch_ms_es<Wifi1296_23>(llr, B, p, bits, soft, used, st);
 }
 #else
-// float early-stop min-sum (qc_ms_es.hip)
+// float early-stop min-sum (qc_es.hip)
 int qc_launch_ms_es_wifi648_12(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
                                int32_t* used, hipStream_t st);
 int qc_launch_ms_es_wifi1296_23(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
@@ -1412,8 +1459,15 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
     const float* x = (const float*)llr;
     float* sf = (float*)soft;
     if (p.algo == LDPC_ALGO_TANH_SP) {
-        if (es) k_qc_sp_st<C, true><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
-        else k_qc_sp_st<C, false><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+        if constexpr (QC_ES_TU != 0) {
+            if (es) {  // qc_es.hip
+                if constexpr (std::is_same_v<C, Wifi648_12>) return qc_launch_ms_es_wifi648_12(llr, B, p, bits, soft, used, st);
+                else return qc_launch_ms_es_wifi1296_23(llr, B, p, bits, soft, used, st);
+            }
+        } else {
+            if (es) k_qc_sp_st<C, true><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+        }
+        if (!es) k_qc_sp_st<C, false><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
     } else if (p.algo == LDPC_ALGO_QMIN_SUM && QC_PACKED != 0) {
         // two codewords per lane in packed fp16 (qc_pk.hip)
         if constexpr (std::is_same_v<C, Wifi648_12>) return qc_launch_qms_pk_wifi648_12(llr, B, p, bits, soft, used, st);
@@ -1436,7 +1490,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
 #undef QL
 #endif
     } else {
-        if constexpr (QC_PHASED != 0 && QC_STORED != 0 && QC_MS_ES_TU != 0) {
+        if constexpr (QC_PHASED != 0 && QC_STORED != 0 && QC_ES_TU != 0) {
             if (es) {
                 if constexpr (std::is_same_v<C, Wifi648_12>) return qc_launch_ms_es_wifi648_12(llr, B, p, bits, soft, used, st);
                 else return qc_launch_ms_es_wifi1296_23(llr, B, p, bits, soft, used, st);
@@ -1445,7 +1499,7 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         const int norm = (p.alpha != 1.0f ? NORM_ALPHA : 0) | (p.beta != 0.0f ? NORM_BETA : 0);
 #define FL(E, N)                                                                                                  \
     do {                                                                                                          \
-        if constexpr (E && QC_PHASED != 0 && QC_STORED != 0 && QC_MS_ES_TU != 0) {                              \
+        if constexpr (E && QC_PHASED != 0 && QC_STORED != 0 && QC_ES_TU != 0) {                              \
         } else if constexpr (QC_PHASED != 0 && C::Z <= 32)                                                      \
             k_qc_ms_ph<C, false, E, N><<<blocks_st, tpb_st, 0, st>>>(x, B, p.iters, p.clamp, p.alpha, p.beta, 0.f, 0.f, 1.f, p.flags, bits, sf, used); \
         else if constexpr (QC_STORED != 0)                                                                        \
@@ -1507,6 +1561,6 @@ int qc_decode(const QCSpec* s, const void* llr, int64_t B, const ldpc_params& p,
               int32_t* used, char*, hipStream_t st) {
     return s->launch_ms(llr, B, p, bits, soft, used, st);
 }
-#endif  // QC_TU_MS_ES
+#endif  // QC_TU_ES
 
 }  // namespace ldpc

@@ -233,7 +233,7 @@ def test_qc_kernel_is_selected(code):
 @pytest.mark.parametrize("snr", [1.0, 2.5, 4.0])
 @pytest.mark.parametrize("alpha,beta", [(0.8125, 0.0), (1.0, 0.0), (1.0, 0.5), (0.8125, 0.5)])
 def test_qc_early_stop_vs_oracle(code, snr, alpha, beta):
-    """Early-stop min-sum, every normalisation (these kernels come from qc_ms_es.hip): iteration counts,
+    """Early-stop min-sum, every normalisation (these kernels come from qc_es.hip): iteration counts,
     bits and z bitwise equal to the oracle; 777 codewords leave the last wave's second codeword empty."""
     H, qc = get_code(code)
     rate = 1 - H.shape[0] / H.shape[1]

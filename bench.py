@@ -10,9 +10,13 @@ data-path exchange, so scaling is weak).
     python bench.py [--gpus N --steps K --warmup W]                  # N=1
     torchrun --nproc-per-node N ... bench.py --gpus N ...            # one rank per GPU
 
-The other BASELINE.json configs are parity-test cases; their throughput lines (profiles/) come from
-the same script, e.g. configs[2]: --code wifi1944_56 --algo tanh --mod 16qam-ofdm --ebn0 4:0.5:9;
-configs[3]: --code wifi1296_23 --algo qminsum --iters 20 --early-stop; configs[4]: --code dvbs2_12 --batch 4096 (EN 302 307 rate-1/2 table).
+The other BASELINE.json configs run as short legs of the same script after the headline, reported under
+``side.configs`` (never ``value``), each event-timed over two launches per Eb/N0 point with its own
+roofline from profiles/counters.json: configs[2] (1944,5/6) tanh-SP 50 it on 16-QAM OFDM LLRs, B=32,768;
+configs[3] (1296,2/3) 5-bit min-sum <=20 it early stop, B=65,536; configs[4] DVB-S2 64800 rate 1/2 min-sum
+50 it, B=4,096 per GPU.  Under torchrun (N>1) the config [4] leg runs on every rank — the BASELINE
+multi-GPU configuration — with its counters summed by the same all-reduce and max-over-ranks timing.
+Any of them alone: e.g. ``--code wifi1944_56 --algo tanh --mod 16qam-ofdm --ebn0 4:0.5:9 --batch 32768``.
 """
 import argparse
 import json
@@ -57,6 +61,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the decode_bits / tanh-SP side measurements")
+    ap.add_argument("--no-legs", action="store_true", help="skip the BASELINE configs[2..4] legs (side.configs)")
+    ap.add_argument("--legs", default="auto",
+                    help="comma list of legs (config2,config3,config4); auto = all three at N=1, config4 at N>1")
+    ap.add_argument("--leg-batch-scale", type=float, default=1.0, help=argparse.SUPPRESS)
     ap.add_argument("--ref-cpu-json", default=os.path.join(ROOT, "profiles", "ref_cpu_wifi648.json"),
                     help="the reference's own CPU decode_bits timing (scripts/time_reference_cpu.py)")
     ap.add_argument("--counters-json", default=os.path.join(ROOT, "profiles", "counters.json"),
@@ -65,10 +73,6 @@ def main():
 
     import torch
     import torch.distributed as dist
-    import ldpc_amd
-    from ldpc_amd import _abi
-    from ldpc_amd.dist import allreduce_counts, max_over_ranks
-    from ldpc_amd.synth import DeviceEncoder
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -84,96 +88,21 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    H, qc = ldpc_amd.get_code(args.code)
-    m, n = H.shape
-    k = n - m
-    rate = k / n
-    dec = ldpc_amd.get_decoder(H, local)
-    B = args.batch
-    lo, step_db, hi = (float(x) for x in args.ebn0.split(":"))
-    ebn0 = np.round(np.arange(lo, hi + 1e-9, step_db), 6)
-    lib = _abi.load()
-    stream = torch.cuda.current_stream()
-    st = stream.cuda_stream
-
-    # ---- synthetic data, resident in HBM before timing -------------------------------------------
-    enc = DeviceEncoder(H, torch.device("cuda", local))
-    info = torch.empty((B, k), dtype=torch.uint8, device="cuda")
-    _abi.check(lib.ldpc_random_bits(info.data_ptr(), B, k, args.seed, rank * B, st))
-    cw = enc.encode(info)
-    llrs = []
-    for i, e in enumerate(ebn0):
-        x = torch.empty((B, n), dtype=torch.float32, device="cuda")
-        if args.mod == "bpsk":
-            sigma = float(np.sqrt(1.0 / (2.0 * rate * 10.0 ** (e / 10.0))))
-            _abi.check(lib.ldpc_awgn_llr(cw.data_ptr(), x.data_ptr(), B, n, sigma, args.seed * 1000 + i, rank * B, st))
-        else:
-            from ldpc_amd.channel import ofdm_demod, ofdm_tx
-            bps = 2 if args.mod == "qpsk-ofdm" else 4
-            esn0 = float(10.0 ** (e / 10.0) * rate * bps)
-            s_ = cw.view(-1)
-            pad = (-s_.numel()) % (bps * 32)
-            if pad:
-                s_ = torch.cat([s_, torch.zeros(pad, dtype=torch.uint8, device="cuda")])
-            rx = ofdm_tx(s_, 32, bps, esn0, args.seed * 1000 + i, rank * B * n // bps)
-            x.copy_(ofdm_demod(rx, 32, bps, esn0)[:B * n].view(B, n))
-        llrs.append(x)
-    p = dec.params(args.iters, args.algo, args.clamp, args.alpha, 0.0, args.early_stop, "f32", "p1",
-                   qstep=args.qstep, force_generic=args.force_generic, device_ptrs=True)
-    wsb = dec.workspace_bytes(B, p)
-    ws = torch.empty((wsb,), dtype=torch.uint8, device="cuda")
-    bits = torch.empty((B, n), dtype=torch.uint8, device="cuda")
-
-    def step(x):
-        _abi.check(lib.ldpc_decode_ex(dec._h, x.data_ptr(), B, p, bits.data_ptr(), None, None, ws.data_ptr(), wsb, st))
-
-    # ---- BER sweep (untimed; also warms up) --------------------------------------------------------
-    counts = torch.zeros((len(ebn0), 3), dtype=torch.int64, device="cuda")
-    for i in range(len(ebn0)):
-        step(llrs[i])
-        _abi.check(lib.ldpc_count_errors(bits.data_ptr(), cw.data_ptr(), B, n, k, counts[i].data_ptr(), st))
-    allreduce_counts(counts)  # the one collective: per-point error counters, 24 B x 11 per rank (RCCL)
-    c = counts.cpu().numpy().astype(np.float64)
-    coded_ber = (c[:, 0] / (c[:, 2] * k)).tolist()
-    coded_bler = (c[:, 1] / c[:, 2]).tolist()
-    for w in range(args.warmup):
-        step(llrs[w % len(ebn0)])
-    torch.cuda.synchronize()
-
-    # ---- timed region -------------------------------------------------------------------------------
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for s in range(args.steps):
-        step(llrs[s % len(ebn0)])
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    gpu_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)
-    my_elapsed = elapsed
-    elapsed = max_over_ranks(elapsed, device="cuda")
+    wl = Workload(args, rank, local)
+    ber = wl.ber()                                       # untimed BER pass over every point (also warms up)
+    elapsed, my_elapsed, gpu_ms = wl.timed(args.steps, args.warmup, world)
+    B, n, E = wl.B, wl.n, wl.E
     total_cw = world * args.steps * B
     ranks = rank_evidence(world, rank, local, my_elapsed)
     value = total_cw / elapsed
-
-    # ---- roofline ---------------------------------------------------------------------------------------
-    E = int(H.sum())  # nnz (SparseCode.sum() too)
-    kpath = "generic-csr" if (args.force_generic or not dec.qc_z) else f"qc-z{dec.qc_z}"
-    roof = roofline(n, E, B, gpu_ms, args, kpath)
+    roof = roofline(n, E, B, gpu_ms, args, wl.kpath)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # CPU baseline at N=1 only
-        cpu = cpu_baseline(H, args, rate)
-    side = None
+        cpu = cpu_baseline(wl.H, args, wl.rate)
+    side = {}
     if rank == 0 and world == 1 and not args.no_dropin and B * n * 8 <= (1 << 32):
-        side = side_measurements(H, dec, llrs[len(ebn0) // 2], B, args)
+        side = side_measurements(wl.H, wl.dec, wl.llrs, B, args, wl.kpath)
         ref = reference_cpu(args)
         if cpu is not None and ref is not None:
             if "value" in ref:
@@ -181,6 +110,16 @@ def main():
                 ref["dropin_over_reference"] = side["dropin"]["cw_per_s"] / ref["value"]
                 ref["headline_over_reference"] = value / ref["value"]
             cpu["reference"] = ref
+    wl.free()
+    # BASELINE.json configs[2..4] (never `value`): at N=1 all three on this GPU; at N>1 config [4] (the
+    # DVB-S2 multi-GPU config) on every rank, its counters reduced by the same all-reduce
+    legs = (list(LEGS) if world == 1 else ["config4"]) if args.legs == "auto" else [x for x in args.legs.split(",") if x]
+    legs = [] if args.no_legs else legs
+    for x in legs:
+        if x not in LEGS:
+            raise SystemExit(f"unknown leg {x!r}; choose from {sorted(LEGS)}")
+    if legs:
+        side["configs"] = {name: run_leg(name, args, rank, local, world) for name in legs}
 
     if rank == 0:
         out = {
@@ -196,27 +135,182 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic: random info bits, systematic encoder, {args.mod} LLRs generated on device",
-            "config": {
-                "workload": f"{args.code} {args.algo} {args.iters} iters{' early-stop' if args.early_stop else ''}, "
-                            f"B={B} codewords/GPU/step, Eb/N0 {args.ebn0} dB cycled per step",
-                "code": args.code, "n": n, "k": k, "edges": E, "algo": args.algo, "iters": args.iters,
-                "clamp": args.clamp, "alpha": args.alpha, "early_stop": args.early_stop, "mod": args.mod,
-                "ebn0": args.ebn0, "seed": args.seed,
-                "batch_per_gpu": B, "global_batch": B * world,
-                "parallelism": f"dp{world} (codeword shards, RCCL all-reduce of error counts only)",
-                "kernel_path": kpath,
-            },
+            "config": wl.config_dict(world),
             "ranks": ranks,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "dropin_cw_per_s": side["dropin"]["cw_per_s"] if side else None,
-            "side": side,
-            "ber": {"ebn0_db": ebn0.tolist(), "coded_ber_info": coded_ber, "coded_bler": coded_bler,
-                    "codewords_per_point": int(c[0, 2])},
+            "dropin_cw_per_s": side["dropin"]["cw_per_s"] if "dropin" in side else None,
+            "side": side or None,
+            "ber": ber,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# BASELINE.json configs[2..4], each one short event-timed leg of this script (side.configs; never `value`)
+LEGS = {
+    "config2": dict(code="wifi1944_56", algo="tanh", iters=50, batch=32768, mod="16qam-ofdm", ebn0="4:0.5:9",
+                    early_stop=False, baseline="configs[2]: tanh sum-product, (1944,5/6), 16-QAM OFDM front end"),
+    "config3": dict(code="wifi1296_23", algo="qminsum", iters=20, batch=65536, mod="bpsk", ebn0="0:0.5:5",
+                    early_stop=True, qstep=1.0,
+                    baseline="configs[3]: 5-bit LLR min-sum, (1296,2/3), 20 iters early termination"),
+    "config4": dict(code="dvbs2_12", algo="minsum", iters=50, batch=4096, mod="bpsk", ebn0="0:0.5:2",
+                    early_stop=False, baseline="configs[4]: DVB-S2 64800 rate 1/2, 50 iters, batch sharded"),
+}
+
+
+def leg_args(name, args):
+    """The bench arguments of one BASELINE leg: this run's defaults (seed, clamp, counters record) with the
+    leg's code / algorithm / batch / front end / Eb/N0 grid."""
+    import argparse as _ap
+    d = dict(vars(args))
+    d.update(force_generic=False, alpha=1.0, qstep=1.0, clamp=20.0)
+    d.update({k: v for k, v in LEGS[name].items() if k != "baseline"})
+    if args.leg_batch_scale != 1.0:  # tests only: a smaller batch (counter records then do not match)
+        d["batch"] = max(64, int(d["batch"] * args.leg_batch_scale))
+    return _ap.Namespace(**d)
+
+
+def run_leg(name, args, rank, local, world):
+    """One BASELINE config as a side leg: data resident in HBM, an untimed BER pass over its grid, one
+    warmup launch, then 2 launches per Eb/N0 point event-timed (so an early-stop leg's mean launch is the
+    sweep's mean), max over ranks; roofline from this leg's own counter record."""
+    import torch
+    la = leg_args(name, args)
+    wl = Workload(la, rank, local)
+    ber = wl.ber()
+    P = len(wl.ebn0)
+    steps = 2 * P
+    elapsed, my_elapsed, gpu_ms = wl.timed(steps, 1, world)
+    rec = {"baseline_config": LEGS[name]["baseline"], "value": world * steps * wl.B / elapsed,
+           "unit": "codewords/s", "n_gpus": world, "steps": steps, "warmup": 1,
+           "ms_per_step": elapsed / steps * 1e3, "ms_per_launch": gpu_ms,
+           "config": wl.config_dict(world), "roofline": roofline(wl.n, wl.E, wl.B, gpu_ms, la, wl.kpath), "ber": ber}
+    if world > 1:
+        rec["ranks"] = rank_evidence(world, rank, local, my_elapsed)
+    wl.free()
+    del wl
+    torch.cuda.empty_cache()
+    return rec
+
+
+class Workload:
+    """One bench configuration on this rank's GPU: the graph, synthetic LLRs for every Eb/N0 point resident
+    in HBM (generated on device from the global codeword index, so the union of the ranks' shards is
+    independent of the world size), decode parameters, workspace and output."""
+
+    def __init__(self, args, rank, local):
+        import torch
+        import ldpc_amd
+        from ldpc_amd import _abi
+        from ldpc_amd.synth import DeviceEncoder
+        self.args, self.rank = args, rank
+        self.H, _ = ldpc_amd.get_code(args.code)
+        m, n = self.H.shape
+        self.n, self.k = n, n - m
+        self.rate = self.k / n
+        self.E = int(self.H.sum())  # nnz (SparseCode.sum() too)
+        self.dec = ldpc_amd.get_decoder(self.H, local)
+        self.kpath = "generic-csr" if (args.force_generic or not self.dec.qc_z) else f"qc-z{self.dec.qc_z}"
+        B = self.B = args.batch
+        lo, step_db, hi = (float(x) for x in args.ebn0.split(":"))
+        self.ebn0 = np.round(np.arange(lo, hi + 1e-9, step_db), 6)
+        self.lib = lib = _abi.load()
+        self.stream = torch.cuda.current_stream()
+        st = self.stream.cuda_stream
+        enc = DeviceEncoder(self.H, torch.device("cuda", local))
+        info = torch.empty((B, self.k), dtype=torch.uint8, device="cuda")
+        _abi.check(lib.ldpc_random_bits(info.data_ptr(), B, self.k, args.seed, rank * B, st))
+        self.cw = enc.encode(info)
+        del info, enc
+        self.llrs = []
+        for i, e in enumerate(self.ebn0):
+            x = torch.empty((B, n), dtype=torch.float32, device="cuda")
+            if args.mod == "bpsk":
+                sigma = float(np.sqrt(1.0 / (2.0 * self.rate * 10.0 ** (e / 10.0))))
+                _abi.check(lib.ldpc_awgn_llr(self.cw.data_ptr(), x.data_ptr(), B, n, sigma, args.seed * 1000 + i,
+                                             rank * B, st))
+            else:
+                from ldpc_amd.channel import ofdm_demod, ofdm_tx
+                bps = 2 if args.mod == "qpsk-ofdm" else 4
+                esn0 = float(10.0 ** (e / 10.0) * self.rate * bps)
+                s_ = self.cw.view(-1)
+                pad = (-s_.numel()) % (bps * 32)
+                if pad:
+                    s_ = torch.cat([s_, torch.zeros(pad, dtype=torch.uint8, device="cuda")])
+                rx = ofdm_tx(s_, 32, bps, esn0, args.seed * 1000 + i, rank * B * n // bps)
+                x.copy_(ofdm_demod(rx, 32, bps, esn0)[:B * n].view(B, n))
+                del rx, s_
+            self.llrs.append(x)
+        self.p = self.dec.params(args.iters, args.algo, args.clamp, args.alpha, 0.0, args.early_stop, "f32", "p1",
+                                 qstep=args.qstep, force_generic=args.force_generic, device_ptrs=True)
+        self.wsb = self.dec.workspace_bytes(B, self.p)
+        self.ws = torch.empty((max(self.wsb, 1),), dtype=torch.uint8, device="cuda")
+        self.bits = torch.empty((B, n), dtype=torch.uint8, device="cuda")
+
+    def step(self, x):
+        from ldpc_amd import _abi
+        _abi.check(self.lib.ldpc_decode_ex(self.dec._h, x.data_ptr(), self.B, self.p, self.bits.data_ptr(), None,
+                                           None, self.ws.data_ptr(), self.wsb, self.stream.cuda_stream))
+
+    def ber(self):
+        """Untimed pass over every point: error counts on device, summed over ranks (the one collective)."""
+        import torch
+        from ldpc_amd import _abi
+        from ldpc_amd.dist import allreduce_counts
+        counts = torch.zeros((len(self.ebn0), 3), dtype=torch.int64, device="cuda")
+        for i in range(len(self.ebn0)):
+            self.step(self.llrs[i])
+            _abi.check(self.lib.ldpc_count_errors(self.bits.data_ptr(), self.cw.data_ptr(), self.B, self.n, self.k,
+                                                  counts[i].data_ptr(), self.stream.cuda_stream))
+        allreduce_counts(counts)  # 24 B x points per rank (RCCL)
+        c = counts.cpu().numpy().astype(np.float64)
+        return {"ebn0_db": self.ebn0.tolist(), "coded_ber_info": (c[:, 0] / (c[:, 2] * self.k)).tolist(),
+                "coded_bler": (c[:, 1] / c[:, 2]).tolist(), "codewords_per_point": int(c[0, 2])}
+
+    def timed(self, steps, warmup, world):
+        """W untimed steps, then exactly K steps cycling over the points, bracketed by a barrier and a device
+        synchronize on both sides.  Returns (max-over-ranks seconds, this rank's seconds, mean event-timed
+        launch ms on the decode stream)."""
+        import torch
+        import torch.distributed as dist
+        from ldpc_amd.dist import max_over_ranks
+        P = len(self.ebn0)
+        for w in range(warmup):
+            self.step(self.llrs[w % P])
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(self.stream)
+        for s in range(steps):
+            self.step(self.llrs[s % P])
+        ev1.record(self.stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        mine = time.perf_counter() - t0
+        gpu_ms = ev0.elapsed_time(ev1) / max(steps, 1)
+        return max_over_ranks(mine, device="cuda"), mine, gpu_ms
+
+    def config_dict(self, world):
+        a = self.args
+        return {"workload": f"{a.code} {a.algo} {a.iters} iters{' early-stop' if a.early_stop else ''}, "
+                            f"B={self.B} codewords/GPU/step, Eb/N0 {a.ebn0} dB cycled per step",
+                "code": a.code, "n": self.n, "k": self.k, "edges": self.E, "algo": a.algo, "iters": a.iters,
+                "clamp": a.clamp, "alpha": a.alpha, "early_stop": a.early_stop, "mod": a.mod,
+                "ebn0": a.ebn0, "seed": a.seed,
+                "batch_per_gpu": self.B, "global_batch": self.B * world,
+                "parallelism": f"dp{world} (codeword shards, RCCL all-reduce of error counts only)",
+                "kernel_path": self.kpath}
+
+    def free(self):
+        self.llrs = []
+        self.cw = self.ws = self.bits = None
 
 
 def rank_evidence(world, rank, local, elapsed):
@@ -298,18 +392,21 @@ def roofline(n, E, B, launch_ms, args, kpath):
     return out
 
 
-def side_measurements(H, dec, llr_dev, B, args):
+def side_measurements(H, dec, llrs, B, args, kpath):
     """Two secondary numbers next to the headline (never `value`):
     * ``dropin``: the reference's boundary itself, ``decode_bits(llrs_f64, H, iters, 256, 10)``
       (ofdm_functions.py:131-163) from host float64 LLRs to host float64 bits — PCIe, staging and the
-      f64<->f32 conversions included (ldpc_decode_bits_host's pinned two-stream pipeline);
+      f64<->f32 conversions included (ldpc_decode_bits_host's pinned two-stream pipeline), at the
+      middle Eb/N0 point;
     * ``gpu_tanh_sp``: the reference's algorithm (tanh sum-product, 50 it, clamp 10) on the same H with
-      LLRs resident in HBM — the apples-to-apples partner of the reference CPU number."""
+      LLRs resident in HBM — the apples-to-apples partner of the reference CPU number.  Timed as the
+      headline is: 3 warmup launches at size, then 2 launches per Eb/N0 point between two HIP events on
+      the decode stream."""
     import torch
     import ldpc_amd
     from ldpc_amd import _abi
     lib = _abi.load()
-    host = llr_dev.double().cpu().numpy()
+    host = llrs[len(llrs) // 2].double().cpu().numpy()
     # graph + staging ring at this size; two calls reach the steady state of a caller's loop
     # (`bits = decode_bits(...)` per SNR point: two output buffers alternate, api._OutputPool)
     for _ in range(2):
@@ -323,24 +420,35 @@ def side_measurements(H, dec, llr_dev, B, args):
               "clamp": 10.0, "batch_size": 256, "bits_set": int(out.sum()),
               "what": "decode_bits(llrs float64 host, H, iters, 256, 10) end to end: f64->f32 staging, "
                       "H2D, decode, D2H, 0/1 float64 expansion"}
+    del host, out
     p = dec.params(args.iters, "tanh", 10.0, device_ptrs=True)
     wsb = dec.workspace_bytes(B, p)
-    ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=llr_dev.device)
-    bits = torch.empty((B, dec.n), dtype=torch.uint8, device=llr_dev.device)
-    st = torch.cuda.current_stream().cuda_stream
-    run = lambda: _abi.check(lib.ldpc_decode_ex(dec._h, llr_dev.data_ptr(), B, p, bits.data_ptr(), None, None,
-                                                ws.data_ptr(), wsb, st))
-    run()
+    dev = llrs[0].device
+    ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device=dev)
+    bits = torch.empty((B, dec.n), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    st = stream.cuda_stream
+
+    def run(x):
+        _abi.check(lib.ldpc_decode_ex(dec._h, x.data_ptr(), B, p, bits.data_ptr(), None, None, ws.data_ptr(), wsb, st))
+    for w in range(3):
+        run(llrs[w % len(llrs)])
     torch.cuda.synchronize()
-    t = time.perf_counter()
-    steps = 3
-    for _ in range(steps):
-        run()
+    steps = 2 * len(llrs)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for s in range(steps):
+        run(llrs[s % len(llrs)])
+    ev1.record(stream)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t) / steps
+    ms = ev0.elapsed_time(ev1) / steps
+    import argparse as _ap
+    targs = _ap.Namespace(**dict(vars(args), algo="tanh", clamp=10.0, early_stop=False))
     return {"dropin": dropin,
-            "gpu_tanh_sp": {"cw_per_s": B / dt, "ms_per_launch": dt * 1e3, "codewords": B, "iters": args.iters,
-                            "clamp": 10.0, "what": "tanh sum-product (the reference's algorithm), LLRs in HBM"}}
+            "gpu_tanh_sp": {"cw_per_s": B / (ms * 1e-3), "ms_per_launch": ms, "launches": steps, "warmup": 3,
+                            "codewords": B, "iters": args.iters, "clamp": 10.0, "timing": "HIP events",
+                            "what": "tanh sum-product (the reference's algorithm), LLRs in HBM",
+                            "roofline": roofline(dec.n, dec.E, B, ms, targs, kpath)}}
 
 
 def reference_cpu(args):

@@ -254,6 +254,10 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
             float a = fabsf(g[d - 1]);
             asm volatile("" : "+v"(a));
             DSet T = {a, 1.0f};
+            if constexpr ((d - 1) % BS == 0) {  // a block ends at hi = d - 1: its T is the last edge alone
+                TD[(d - 1) / BS - 1] = T.D;
+                TS[(d - 1) / BS - 1] = T.S;
+            }
             static_for<0, d - 1 - BS>([&](auto uu) __attribute__((always_inline)) {
                 constexpr int t = d - 2 - decltype(uu)::value;  // d-2 down to BS
                 float b = fabsf(g[t]);

@@ -1197,6 +1197,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 // row by row with an early exit (as the min-sum kernels): the columns' hard decisions packed in
                 // one register, then each row's parity from ballots of its columns' bits until no codeword of
                 // the wave can still be satisfied
+                static_assert(NB <= 32, "one hard-decision bit per block column in a 32-bit word");
                 uint32_t hd = 0;
                 static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
                     constexpr int j = decltype(jj)::value;

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import hashlib
+import os
 import threading
 
 import numpy as np
@@ -256,18 +257,37 @@ class _OutputPool:
     drops it (and every view of it), a ``weakref.finalize`` on its per-call buffer exporter puts the buffer
     back, and a later call of the same size reuses it: the library rewrites every decoded row and the tail
     rows are zeroed, so each result is indistinguishable from a fresh ``np.zeros`` one.  At most ``keep`` free
-    buffers of at most ``max_bytes`` in total are held (the oldest are released first)."""
+    buffers of at most ``max_bytes`` in total are held (the oldest are released first).
+
+    The finalizer can run inside ANY allocation on this thread (the cyclic GC frees an array that sat in a
+    reference cycle), including while ``array()`` holds the pool's lock, so it takes no lock: it only appends
+    to a deque (atomic), and ``array()`` folds the returned buffers into the free list under the lock."""
 
     def __init__(self, keep=2, max_bytes=2 << 30):
+        import collections
         self.keep, self.max_bytes = keep, max_bytes
-        self._free = []          # [(nbytes, 1-D float64 buffer)], oldest first
+        self._free = []          # [(nbytes, 1-D float64 buffer)], oldest first; guarded by _lock
+        self._returned = collections.deque()   # buffers handed back by finalizers (lock-free append)
         self._lock = threading.Lock()
 
     def _release(self, buf):
-        with self._lock:
+        self._returned.append(buf)   # no lock, no allocation beyond the deque slot: safe inside a GC pass
+
+    def _fold(self):
+        """Move returned buffers into the free list, oldest first, trimming to the limits (lock held)."""
+        while True:
+            try:
+                buf = self._returned.popleft()
+            except IndexError:
+                break
             self._free.append((buf.nbytes, buf))
-            while len(self._free) > self.keep or sum(b for b, _ in self._free) > self.max_bytes:
-                self._free.pop(0)
+        while len(self._free) > self.keep or sum(b for b, _ in self._free) > self.max_bytes:
+            self._free.pop(0)
+
+    def free_count(self):
+        with self._lock:
+            self._fold()
+            return len(self._free)
 
     def array(self, shape, rows):
         """(shape) float64 array whose rows >= ``rows`` are zero; rows < ``rows`` are for the caller to fill."""
@@ -275,6 +295,7 @@ class _OutputPool:
         count = int(np.prod(shape))
         buf = None
         with self._lock:
+            self._fold()
             for i, (nb, b) in enumerate(self._free):
                 if b.size == count:
                     buf = self._free.pop(i)[1]
@@ -295,13 +316,21 @@ class _OutputPool:
 _outputs = _OutputPool()
 
 
-def decode_bits(llrs, H, bp_iterations, batch_size, clamp_value):
+def decode_bits(llrs, H, bp_iterations, batch_size, clamp_value, *, fresh_output=None):
     """Drop-in for ``decode_bits`` (``pytorch/ofdm/ofdm_functions.py:131-163``).
 
     Same arguments and conventions: ``llrs`` (N, n) in log P(1)/P(0), converted to float32 as the
     reference does (``:156``); tanh sum-product for ``bp_iterations`` flooding iterations with messages
     clamped to ``clamp_value``; returns float64 0.0/1.0 of shape (N, n) where only the first
     ``(N // batch_size) * batch_size`` rows are decoded and the remainder stays 0 (``:133-135``).
+
+    Output ownership: by default the result is a numpy array over a RECYCLED buffer (``_OutputPool``):
+    ``out.flags.owndata`` is False (its ``.base`` is a ctypes exporter), so ``out.resize()`` raises, and
+    once the caller has dropped the array and every view of it, a later call may rewrite that memory — a
+    raw pointer kept past that point (``out.ctypes.data``) is not owned.  Values, shape, dtype and
+    writeability are those of the reference's fresh ``np.zeros`` result.  ``fresh_output=True`` (or the
+    environment variable ``LDPC_FRESH_OUTPUT=1``) returns a freshly allocated, self-owning array instead,
+    as the reference does, at the cost of populating new pages on every call.
     """
     llrs = np.asarray(llrs)
     num_batches = llrs.shape[0] // batch_size  # ZeroDivisionError for batch_size == 0, as the reference
@@ -310,6 +339,8 @@ def decode_bits(llrs, H, bp_iterations, batch_size, clamp_value):
         output_bits = np.zeros(llrs.shape)
         if rows == 0:
             return output_bits
+    elif fresh_output or (fresh_output is None and os.environ.get("LDPC_FRESH_OUTPUT", "") not in ("", "0")):
+        output_bits = np.zeros(llrs.shape)
     else:
         output_bits = _outputs.array(llrs.shape, rows)  # rows >= `rows` zero; the library writes the rest
     hshape = H.shape if isinstance(H, SparseCode) else np.asarray(H).shape

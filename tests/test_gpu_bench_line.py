@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_bench_line_contract():
     out = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--batch", "8192",
-                          "--cpu-seconds", "0.5"], cwd=ROOT, capture_output=True, text=True, timeout=300)
+                          "--cpu-seconds", "0.5", "--leg-batch-scale", "0.0625"], cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
@@ -35,3 +35,20 @@ def test_bench_line_contract():
     assert d["side"]["gpu_tanh_sp"]["cw_per_s"] > 0 and d["dropin_cw_per_s"] > 0
     assert d["ranks"]["world_size"] == 1 and len(d["ranks"]["per_rank"]) == 1
     assert len(d["ber"]["ebn0_db"]) == 11 and d["ber"]["codewords_per_point"] == 8192
+    assert d["side"]["gpu_tanh_sp"]["timing"] == "HIP events" and d["side"]["gpu_tanh_sp"]["launches"] >= 20
+    # BASELINE configs[2..4] as side legs (never `value`), each event-timed with its own roofline
+    legs = d["side"]["configs"]
+    assert sorted(legs) == ["config2", "config3", "config4"]
+    want = {"config2": ("wifi1944_56", "tanh", 50, "16qam-ofdm", False, 2048),
+            "config3": ("wifi1296_23", "qminsum", 20, "bpsk", True, 4096),
+            "config4": ("dvbs2_12", "minsum", 50, "bpsk", False, 256)}
+    for name, (code, algo, iters, mod, es, b) in want.items():
+        lg = legs[name]
+        c = lg["config"]
+        assert (c["code"], c["algo"], c["iters"], c["mod"], c["early_stop"], c["batch_per_gpu"]) == \
+            (code, algo, iters, mod, es, b), name
+        P = len(lg["ber"]["ebn0_db"])
+        assert lg["steps"] == 2 * P and lg["value"] > 0 and lg["ms_per_launch"] > 0
+        assert abs(lg["value"] - b / (lg["ms_per_step"] / 1e3)) <= 1e-6 * lg["value"]
+        for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_ms"):
+            assert k in lg["roofline"], (name, k)

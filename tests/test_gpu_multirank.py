@@ -58,7 +58,7 @@ def _bench_line(out):
 
 def test_bench_two_ranks_equal_one_process_over_both_shards():
     common = ["bench.py", "--steps", "2", "--warmup", "1", "--iters", "10", "--ebn0", "1:1:3",
-              "--no-cpu-baseline"]
+              "--no-cpu-baseline", "--no-legs"]
     two = _bench_line(_launch([*common, "--gpus", "2", "--batch", "4096"], 2))
     one = _bench_line(_launch([*common, "--gpus", "1", "--batch", "8192"], 1))
     assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 8192 and two["value"] > 0
@@ -98,3 +98,28 @@ def test_bench_dvbs2_config4_two_ranks_equal_one_process():
     assert two["ber"]["coded_ber_info"] == one["ber"]["coded_ber_info"]
     assert two["ber"]["coded_bler"] == one["ber"]["coded_bler"]
     assert one["ber"]["coded_bler"][0] > 0 and one["ber"]["coded_bler"][-1] < one["ber"]["coded_bler"][0]
+
+
+def test_bench_multigpu_runs_the_config4_leg():
+    """At N>1 bench.py also runs BASELINE config [4] (DVB-S2 64800 rate 1/2, 50 min-sum iterations) on every
+    rank — the multi-GPU configuration BASELINE names — under side.configs.config4, with max-over-ranks
+    timing, every rank's timed seconds in its ``ranks`` and the counters summed by the all-reduce: equal to
+    one process decoding both shards (here 256 codewords per rank through --leg-batch-scale)."""
+    common = ["bench.py", "--steps", "1", "--warmup", "0", "--iters", "5", "--batch", "1024", "--ebn0", "1:1:2",
+              "--no-cpu-baseline", "--no-dropin"]
+    two = _bench_line(_launch([*common, "--gpus", "2", "--leg-batch-scale", "0.0625"], 2, timeout=400))
+    one = _bench_line(_launch([*common, "--gpus", "1", "--legs", "config4", "--leg-batch-scale", "0.125"], 1,
+                              timeout=400))
+    l2, l1 = two["side"]["configs"]["config4"], one["side"]["configs"]["config4"]
+    assert list(two["side"]["configs"]) == ["config4"] and list(one["side"]["configs"]) == ["config4"]
+    assert l2["n_gpus"] == 2 and l2["config"]["code"] == "dvbs2_12" and l2["config"]["iters"] == 50
+    assert l2["config"]["batch_per_gpu"] == 256 and l2["config"]["global_batch"] == 512
+    assert l2["config"]["kernel_path"] == "generic-csr"
+    rk = l2["ranks"]
+    assert rk["world_size"] == 2 and [r["rank"] for r in rk["per_rank"]] == [0, 1]
+    assert all(r["timed_s"] > 0 for r in rk["per_rank"])
+    assert abs(l2["value"] - 2 * l2["steps"] * 256 / (l2["ms_per_step"] * l2["steps"] / 1e3)) <= 1e-6 * l2["value"]
+    assert l2["ber"]["codewords_per_point"] == l1["ber"]["codewords_per_point"] == 512
+    assert l2["ber"]["coded_ber_info"] == l1["ber"]["coded_ber_info"]
+    assert l2["ber"]["coded_bler"] == l1["ber"]["coded_bler"]
+    assert l2["roofline"]["bound"] == "hbm" and l2["roofline"]["frac"] > 0

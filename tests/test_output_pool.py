@@ -34,6 +34,35 @@ def test_pool_bounds():
     arrs = [pool.array((10, 8), 10) for _ in range(3)]
     del arrs
     gc.collect()
-    assert len(pool._free) == 1
+    assert pool.free_count() == 1
     big = pool.array((100, 100), 0)                # larger than max_bytes: a plain np.zeros, not pooled
     assert not big.any() and big.shape == (100, 100)
+
+
+def test_release_from_gc_inside_the_lock_does_not_deadlock():
+    """an array in a reference cycle is freed by the cyclic GC, which can run on the thread that
+    already holds the pool's lock (inside array()).  The finalizer must not take that lock."""
+    import threading
+    pool = _OutputPool(keep=2, max_bytes=1 << 26)
+    done = threading.Event()
+
+    def body():
+        a = pool.array((6, 4), 6)
+        cyc = [a]
+        cyc.append(cyc)                 # a reference cycle: only the cyclic GC frees `a`
+        del a, cyc
+        with pool._lock:                # as inside array(): the GC pass runs with the lock held
+            gc.collect()
+        done.set()
+
+    gc.disable()
+    try:
+        t = threading.Thread(target=body, daemon=True)
+        t.start()
+        t.join(10)
+    finally:
+        gc.enable()
+    assert done.is_set(), "finalizer deadlocked on the pool lock"
+    assert pool.free_count() == 1        # the buffer came back through the lock-free path
+    b = pool.array((6, 4), 2)
+    assert not b[2:].any()

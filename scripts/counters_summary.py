@@ -5,11 +5,11 @@ per-launch MEAN counters of the decode and the derived roofline fractions.
     python scripts/counters_summary.py gpurun_out/prof_headline --name headline --kernel k_qc_ms
     python scripts/counters_summary.py gpurun_out/prof_c4 --name c4 --decode-kernels k_load_llr,k_vn_,k_cn_,k_final
 
-Which launches: every profiling pass runs bench.py with ``--steps P --warmup 0`` (P = the number of Eb/N0
-points), i.e. the untimed BER pass and the timed loop each launch the decode ONCE PER POINT.  The record
-holds the mean over all those launches — each point weighted equally, as in bench's event-timed mean over
-a whole number of sweeps — and the kernel-trace pass runs the same arguments, so its mean duration is over
-the same launches.  (Round 3 took the median over a 4-step run: for an early-stop kernel that is one
+Which launches: every profiling pass runs bench.py with ``--steps P --warmup P`` (P = the number of Eb/N0
+points): the untimed BER pass, the warmup and the timed loop each launch the decode ONCE PER POINT.  With
+``--last P`` the record holds the mean over the timed loop's P launches — each point weighted equally, as in
+bench's event-timed mean over a whole number of sweeps, after the clock has ramped — and the kernel-trace
+pass runs the same arguments, so its mean duration is over the same launches.  (Round 3 took the median over a 4-step run: for an early-stop kernel that is one
 non-converging launch, not the sweep.)  ``--kernel`` names one decode kernel (the register kernels decode
 in one launch); ``--decode-kernels`` lists the kernels of a multi-launch decode (generic CSR path): their
 counts and durations are summed per decode, decodes = dispatches of the first one.
@@ -20,8 +20,8 @@ Derivations (MI355X_MICROARCH.md):
 * LDS pipe: SQ_LDS_IDX_ACTIVE = LDS-array cycles summed over the 256 CUs. lds_frac = LDS_IDX_ACTIVE / (256 * cycles).
 * cycles = GRBM_GUI_ACTIVE / 8: the counter is reported summed over the 8 XCDs (it reads 8 x the launch
   duration x the shader clock).  The clock it implies (cycles / mean kernel-trace duration) must not exceed
-  the 2.4 GHz peak engine clock: a record that implies more counted other launches than it timed and is
-  REJECTED (exit status 2).
+  the 2.4 GHz peak engine clock (1 % tolerance: trace timestamps vs the counter's window on the same
+  launches): a record that implies more counted other launches than it timed and is REJECTED.
 * HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE (KB; gfx950 FETCH_SIZE counts half the coalesced read bytes;
   re-calibrated in the same pass on k_awgn, whose reads/writes are known exactly).
 bench.py reads these per-launch counts and divides them by its live event-timed launch duration.
@@ -35,53 +35,77 @@ import statistics
 
 XCDS, SIMDS, CUS = 8, 1024, 256
 MAX_CLOCK_GHZ = 2.4
+CLOCK_TOL = 1.01  # the trace's timestamps and the counter's GRBM window differ by < 1 % on matching launches
 
 
 def per_kernel(path):
-    """{(kernel name, counter): [value per dispatch]} over every PMC pass under ``path``."""
+    """{(kernel name, counter): [[(dispatch id, value)] per PMC pass]} over every pass under ``path`` (each
+    pass is its own process, so dispatch ids repeat across passes and are only ordered within one)."""
     vals = {}
-    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+    for f in sorted(glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)):
+        mine = {}
         for r in csv.DictReader(open(f)):
-            vals.setdefault((r["Kernel_Name"], r["Counter_Name"]), []).append(float(r["Counter_Value"]))
+            mine.setdefault((r["Kernel_Name"], r["Counter_Name"]), []).append((int(r["Dispatch_Id"]),
+                                                                                float(r["Counter_Value"])))
+        for k, v in mine.items():
+            vals.setdefault(k, []).append(sorted(v))
     return vals
 
 
 def trace_durations(path):
-    """{kernel name: [duration ms per dispatch]} from the kernel-trace pass."""
+    """{kernel name: [(dispatch id, duration ms)]} from the kernel-trace pass."""
     out = {}
     for f in glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True):
         for t in csv.DictReader(open(f)):
-            out.setdefault(t["Kernel_Name"], []).append((int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e6)
-    return out
+            out.setdefault(t["Kernel_Name"], []).append(
+                (int(t["Dispatch_Id"]), (int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e6))
+    return {k: sorted(v) for k, v in out.items()}
 
 
-def summarise(vals, durs, kernel=None, decode_kernels=None):
-    """Per-decode counters and duration.  Returns (kernel label, counters, kstats)."""
+def _tail(rows, last):
+    return [v for _, v in rows[-last:]] if last else [v for _, v in rows]
+
+
+def summarise(vals, durs, kernel=None, decode_kernels=None, last=0):
+    """Per-decode counters and duration over the last ``last`` decodes of each pass (0: all), averaged over
+    the passes that collected the counter.  Returns (label, counters, kstats)."""
     if kernel:
         names = {k for (k, _) in vals if kernel in k}
         if not names:
             raise SystemExit(f"no kernel matching {kernel}")
-        kname = max(names, key=lambda k: len(vals.get((k, "SQ_INSTS_VALU"), vals.get((k, "FETCH_SIZE"), []))))
-        c = {cn: statistics.fmean(v) for (k, cn), v in vals.items() if k == kname}
-        d = durs.get(kname, [])
+        kname = max(names, key=lambda k: sum(map(len, vals.get((k, "SQ_INSTS_VALU"), vals.get((k, "FETCH_SIZE"), [])))))
+        c = {cn: statistics.fmean(statistics.fmean(_tail(rows, last)) for rows in passes)
+             for (k, cn), passes in vals.items() if k == kname}
+        d = _tail(durs.get(kname, []), last)
         ks = {"kernel": kname.split("(")[0], "calls": len(d), "mean_ms": statistics.fmean(d) if d else None,
               "min_ms": min(d) if d else None, "max_ms": max(d) if d else None}
         return kname.split("(")[0], c, ks
     pats = decode_kernels.split(",")
-    first = [k for k in durs if pats[0] in k]
-    if not first:
-        raise SystemExit(f"no kernel matching {pats[0]} in the kernel trace")
-    n_dec = sum(len(durs[k]) for k in first)
+
+    def per_decode(rows_by_kernel):
+        """(sum over the decode kernels of their values in the last `last` decodes) / decodes, for one pass;
+        a decode starts at a dispatch of the first pattern's kernel"""
+        ids = sorted(i for k, rows in rows_by_kernel.items() if pats[0] in k for i, _ in rows)
+        if not ids:
+            raise SystemExit(f"no kernel matching {pats[0]}")
+        start, n_dec = (ids[-last], min(last, len(ids))) if last else (ids[0], len(ids))
+        tot = sum(v for k, rows in rows_by_kernel.items() if any(p in k for p in pats) for i, v in rows if i >= start)
+        return tot / n_dec, start, n_dec
     c = {}
-    for (k, cn), v in vals.items():
+    for cn in {cn for (_, cn) in vals}:
+        npass = max(len(p) for (k, c2), p in vals.items() if c2 == cn)
+        per_pass = []
+        for ip in range(npass):
+            by_k = {k: p[ip] for (k, c2), p in vals.items() if c2 == cn and ip < len(p)}
+            per_pass.append(per_decode(by_k)[0])
+        c[cn] = statistics.fmean(per_pass)
+    tot_ms, start, n_dec = per_decode(durs)
+    per = {}
+    for k, rows in durs.items():
         if any(p in k for p in pats):
-            c[cn] = c.get(cn, 0.0) + sum(v)
-    n_dec_pmc = sum(len(v) for (k, cn), v in vals.items() if pats[0] in k and cn in ("FETCH_SIZE", "SQ_INSTS_VALU"))
-    n_pmc = {cn: sum(len(v) for (k, c2), v in vals.items() if pats[0] in k and c2 == cn) for cn in c}
-    c = {cn: tot / max(n_pmc.get(cn, 0) or n_dec_pmc or 1, 1) for cn, tot in c.items()}
-    tot_ms = sum(sum(v) for k, v in durs.items() if any(p in k for p in pats))
-    ks = {"kernel": "+".join(pats), "calls": n_dec, "mean_ms": tot_ms / n_dec if n_dec else None,
-          "per_kernel_ms": {k.split("(")[0]: statistics.fmean(v) for k, v in durs.items() if any(p in k for p in pats)}}
+            sel = [v for i, v in rows if i >= start]
+            per[k.split("(")[0]] = {"calls": len(sel), "mean_ms": statistics.fmean(sel) if sel else None}
+    ks = {"kernel": "+".join(pats), "calls": n_dec, "mean_ms": tot_ms, "per_kernel": per}
     return ks["kernel"], c, ks
 
 
@@ -92,19 +116,20 @@ def main():
     ap.add_argument("--kernel")
     ap.add_argument("--decode-kernels")
     ap.add_argument("--max-clock-ghz", type=float, default=MAX_CLOCK_GHZ)
+    ap.add_argument("--last", type=int, default=0, help="use the last N decodes of each pass (the timed loop)")
     a = ap.parse_args()
     if bool(a.kernel) == bool(a.decode_kernels):
         raise SystemExit("give exactly one of --kernel / --decode-kernels")
     bench = json.load(open(os.path.join(a.dir, "bench.json")))
     vals = per_kernel(a.dir)
     durs = trace_durations(os.path.join(a.dir, "ks"))
-    label, c, ks = summarise(vals, durs, a.kernel, a.decode_kernels)
+    label, c, ks = summarise(vals, durs, a.kernel, a.decode_kernels, a.last)
     cfg = bench["config"]
     rec = {"name": a.name, "kernel": label,
            "config": {k: cfg.get(k) for k in ("code", "algo", "iters", "early_stop", "batch_per_gpu", "mod", "kernel_path",
                                               "ebn0", "seed")},
-           "launches": "one decode per Eb/N0 point in the BER pass and again in the timed loop (--steps P --warmup 0); "
-                       "counters and kernel-trace duration are means over the same launches",
+           "launches": f"the timed loop of `--steps P --warmup P` (P = Eb/N0 points): the last {a.last} decodes, one per "
+                       "point; counters and kernel-trace duration are means over the same launches",
            "bench": {"value": bench["value"], "ms_per_step": bench["ms_per_step"],
                      "launch_ms_events": bench["roofline"]["launch_ms"]},
            "kernel_stats": ks, "counters_per_launch": c}
@@ -128,10 +153,10 @@ def main():
         d["hbm_bytes"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
         aw = [k for (k, cn) in vals if "k_awgn" in k and cn == "FETCH_SIZE"]
         if aw:
-            d["awgn_fetch_kb_x2"] = 2 * statistics.fmean(vals[(aw[0], "FETCH_SIZE")])
-            d["awgn_write_kb"] = statistics.fmean(vals[(aw[0], "WRITE_SIZE")])
+            d["awgn_fetch_kb_x2"] = 2 * statistics.fmean(_tail(vals[(aw[0], "FETCH_SIZE")][0], 0))
+            d["awgn_write_kb"] = statistics.fmean(_tail(vals[(aw[0], "WRITE_SIZE")][0], 0))
     rec["derived"] = d
-    if d.get("clock_ghz", 0.0) > a.max_clock_ghz:
+    if d.get("clock_ghz", 0.0) > a.max_clock_ghz * CLOCK_TOL:
         raise SystemExit(f"REJECTED {a.name}: implied clock {d['clock_ghz']:.3f} GHz > {a.max_clock_ghz} GHz — the "
                          f"counted launches are not the timed ones")
     print(json.dumps(rec, indent=1))

@@ -29,6 +29,7 @@ bench.py reads these per-launch counts and divides them by its live event-timed 
 import argparse
 import csv
 import glob
+import gzip
 import json
 import os
 import statistics
@@ -42,9 +43,11 @@ def per_kernel(path):
     """{(kernel name, counter): [[(dispatch id, value)] per PMC pass]} over every pass under ``path`` (each
     pass is its own process, so dispatch ids repeat across passes and are only ordered within one)."""
     vals = {}
-    for f in sorted(glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)):
+    files = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
+    files += glob.glob(os.path.join(path, "**", "*counter_collection.csv.gz"), recursive=True)  # committed copies
+    for f in sorted(files):
         mine = {}
-        for r in csv.DictReader(open(f)):
+        for r in csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)):
             mine.setdefault((r["Kernel_Name"], r["Counter_Name"]), []).append((int(r["Dispatch_Id"]),
                                                                                 float(r["Counter_Value"])))
         for k, v in mine.items():
@@ -92,7 +95,7 @@ def summarise(vals, durs, kernel=None, decode_kernels=None, last=0):
         tot = sum(v for k, rows in rows_by_kernel.items() if any(p in k for p in pats) for i, v in rows if i >= start)
         return tot / n_dec, start, n_dec
     c = {}
-    for cn in {cn for (_, cn) in vals}:
+    for cn in sorted({cn for (_, cn) in vals}):
         npass = max(len(p) for (k, c2), p in vals.items() if c2 == cn)
         per_pass = []
         for ip in range(npass):
@@ -156,7 +159,10 @@ def main():
             d["awgn_fetch_kb_x2"] = 2 * statistics.fmean(_tail(vals[(aw[0], "FETCH_SIZE")][0], 0))
             d["awgn_write_kb"] = statistics.fmean(_tail(vals[(aw[0], "WRITE_SIZE")][0], 0))
     rec["derived"] = d
-    if d.get("clock_ghz", 0.0) > a.max_clock_ghz * CLOCK_TOL:
+    # a multi-launch decode (~500 dispatches) adds each dispatch's few us of front-end time to the counter's
+    # window but not to the kernels' traced durations: 3 % there
+    tol = CLOCK_TOL if a.kernel else 1.03
+    if d.get("clock_ghz", 0.0) > a.max_clock_ghz * tol:
         raise SystemExit(f"REJECTED {a.name}: implied clock {d['clock_ghz']:.3f} GHz > {a.max_clock_ghz} GHz — the "
                          f"counted launches are not the timed ones")
     print(json.dumps(rec, indent=1))

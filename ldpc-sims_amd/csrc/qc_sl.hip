@@ -180,6 +180,8 @@ static int launch_sl(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         if (es) {
             static_assert(std::is_same_v<C, Wifi1944_56>, "one sliced code");
             qc_launch_sp_sl_es_wifi1944_56(x, B, p, bits, sf, used, st);
+        } else if (QC_SL_SP_RS) {
+            k_qc_sp_rs<C><<<blocks, tb, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
         } else {
             k_qc_sp_sl<C, false><<<blocks, tb, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
         }

@@ -300,4 +300,237 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     if (valid && k == 0 && l == 0 && iters_used) iters_used[cw] = h ? used1 : used0;
 }
 
+// ---- resident sliced tanh-SP (config [2]: 802.11n (1944,5/6), Z = 81) ------------------------------
+// k_qc_sp_sl above keeps every message in VGPRs and exchanges the rotated circulants' values through an LDS
+// row per block row: three or four barriers per block row (16 per iteration), SQ_WAIT_ANY 0.39.  Here the
+// messages of the ROTATED circulants live in LDS for the whole decode, one 32-bit slot per (edge, position),
+// updated in place: the VN phase reads every column's c2v, forms its v2c and writes them back at the same
+// slots; a barrier; the CN phase reads every row's v2c, forms its c2v and writes them back; a barrier — two
+// barriers per iteration.  Each slot is touched by exactly one lane in each phase (its variable's owner in
+// the VN phase, its check's owner in the CN phase), so in place is race-free between the two barriers.
+// Rotation-0 circulants (30 of 79) keep their messages in VGPRs as before.
+// Addressing without a per-access modulo: circulant (r, t) with rotation rho = Q*a + b (Q = 9 for Z = 81)
+// stores check position p at slot (p + Q*a) mod Z of its row of Z floats; the check's owner (position p)
+// reads slot (p + Q*a) mod Z and the variable's owner (position z = p + rho) slot (z - b) mod Z — the same
+// slot.  Each lane precomputes its byte address for the Z/Q values of a and the Q values of b once (17
+// VGPRs for Z = 81, where every rotation would need its own: 42); the circulant's row offset rides in the
+// ds instruction's immediate.  LDS: 49 rotated circulants x 2 codewords x 81 x 4 B = 31.0 KiB per unit of
+// three waves, five units (15 waves) per CU, as the register-exchange kernel.  Arithmetic operation for
+// operation that kernel's (bitwise equal results; tests/test_gpu_parity.py).
+#ifndef QC_SL_SP_RS
+#define QC_SL_SP_RS 1
+#endif
+#ifndef QC_RS_WAVES_PER_SIMD
+#define QC_RS_WAVES_PER_SIMD 4
+#endif
+#ifndef QC_RS_SERIAL
+#define QC_RS_SERIAL 1  // the VN chains' ties (vn_excl_sums' TIE)
+#endif
+#ifndef QC_RS_SERIAL_ROW
+#define QC_RS_SERIAL_ROW 1  // the check rows' ties (cn_ds_row's SERIAL); 2: 59 VGPRs spilled
+#endif
+#ifndef QC_RS_ADDR_OPAQUE
+#define QC_RS_ADDR_OPAQUE 1  // address VGPRs passed through an empty asm at each use (a v_mov each)
+#endif
+#ifndef QC_RS_L
+#define QC_RS_L 2  // where L lives: 0 VGPRs (loaded once), 2 re-read from global memory at every use
+#endif
+
+template <class C>
+constexpr int rs_rot_index(int r, int t) {  // index of circulant (r, t) among the rotated ones, check order
+    int c = 0;
+    for (int q = 0; q < C::MB; ++q)
+        for (int u = 0; u < C::DEG[q]; ++u) {
+            if (q == r && u == t) return c;
+            c += (C::SHR[q][u] != 0);
+        }
+    return -1;
+}
+template <class C>
+constexpr int rs_zero_index(int r, int t) {  // index of circulant (r, t) among the rotation-0 ones
+    int c = 0;
+    for (int q = 0; q < C::MB; ++q)
+        for (int u = 0; u < C::DEG[q]; ++u) {
+            if (q == r && u == t) return c;
+            c += (C::SHR[q][u] == 0);
+        }
+    return -1;
+}
+template <class C>
+constexpr int rs_rot_total() {
+    return rs_rot_index<C>(C::MB - 1, C::DEG[C::MB - 1] - 1) + (C::SHR[C::MB - 1][C::DEG[C::MB - 1] - 1] != 0);
+}
+template <int Z>
+constexpr int rs_q() {  // the smallest Q with Q * Q >= Z (9 for 81)
+    int q = 1;
+    while (q * q < Z) ++q;
+    return q;
+}
+
+template <class C>
+__global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_RS_WAVES_PER_SIMD)))
+void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
+                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
+    constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
+    constexpr int NE = edge_off<C>(MB), NR = rs_rot_total<C>(), N0 = NE - NR;
+    constexpr int Q = rs_q<Z>(), NA = (Z - 1) / Q + 1;
+    constexpr int CROW = 2 * Z * 4;  // bytes per rotated circulant: [half][position]
+    static_assert(S > 1 && Z % S == 0 && ZL <= 32, "sliced kernel: Z = S * ZL, ZL <= 32");
+    static_assert(NR * CROW < 65536, "circulant offsets ride in the 16-bit ds offset");
+    __shared__ float X[NR * 2 * Z];
+    char* const Xb = reinterpret_cast<char*>(X);
+    const int k = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // slot of this wave
+    const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
+    const int64_t cw = (int64_t)blockIdx.x * 2 + h;
+    const bool live = l < ZL;                // lane carries a frame position (stores are live lanes only)
+    const bool valid = live && cw < B;
+    // idle lanes read at their wave's first position (a broadcast, see k_qc_sp_sl) and never store
+    const int zc = live ? l + ZL * k : ZL * k;
+    // byte addresses of this lane's slot for a = 0 .. NA-1 (check side) and b = 0 .. Q-1 (variable side)
+    int aC[NA], aV[Q];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+        int p = zc + Q * a;
+        p -= (p >= Z) ? Z : 0;
+        aC[a] = 4 * (h * Z + p);
+    }
+#pragma unroll
+    for (int b = 0; b < Q; ++b) {
+        int p = zc - b;
+        p += (p < 0) ? Z : 0;
+        aV[b] = 4 * (h * Z + p);
+    }
+    // slot of edge (r, t) seen from the check side / the variable side (compile-time rotation, runtime base)
+    auto cref = [&](auto rr, auto tt) __attribute__((always_inline)) -> float& {
+        constexpr int r = decltype(rr)::value, t = decltype(tt)::value, s = C::SHR[r][t];
+        int a = aC[s / Q];
+        if constexpr (QC_RS_ADDR_OPAQUE) asm volatile("" : "+v"(a));  // one address VGPR per value of a
+        return *reinterpret_cast<float*>(Xb + a + rs_rot_index<C>(r, t) * CROW);
+    };
+    auto vref = [&](auto rr, auto tt) __attribute__((always_inline)) -> float& {
+        constexpr int r = decltype(rr)::value, t = decltype(tt)::value, s = C::SHR[r][t];
+        int a = aV[s % Q];
+        if constexpr (QC_RS_ADDR_OPAQUE) asm volatile("" : "+v"(a));
+        return *reinterpret_cast<float*>(Xb + a + rs_rot_index<C>(r, t) * CROW);
+    };
+    // L = -llr (bp.py:47) of this lane's variable in block column j: in VGPRs, or re-read at every use (L2)
+    const float* const lp = llr + (valid ? cw * N : 0);
+    float Lreg[QC_RS_L == 0 ? NB : 1];
+    auto Lload = [&](int j, bool opaque) __attribute__((always_inline)) {
+        int z = zc;
+        if (opaque) asm volatile("" : "+v"(z));
+        int t = z + C::PHI[j];
+        t -= (t >= Z) ? Z : 0;
+        return valid ? -lp[j * Z + t] : 0.0f;
+    };
+    if constexpr (QC_RS_L == 0) {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) Lreg[j] = Lload(j, false);
+    }
+    auto Lr_at = [&](int j) __attribute__((always_inline)) {
+        if constexpr (QC_RS_L == 0) return Lreg[j];
+        else return Lload(j, true);
+    };
+    float m0[N0 > 0 ? N0 : 1];  // messages of the rotation-0 circulants (both frames agree)
+#pragma unroll
+    for (int e = 0; e < N0; ++e) m0[e] = 0.0f;
+    if (live) {  // c2v = 0 before the first iteration (bp.py:46: x = 0); each lane zeroes its check slots
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            static_for<0, C::DEG[decltype(rr)::value]>([&](auto tt) __attribute__((always_inline)) {
+                if constexpr (C::SHR[decltype(rr)::value][decltype(tt)::value] != 0) cref(rr, tt) = 0.0f;
+            });
+        });
+    }
+    __syncthreads();
+    const float cmax2 = sp_cmax2(clamp);  // check outputs in log2 units (common.h)
+    // column j's messages in ascending row order: (row, slot) of its k-th edge
+    auto col_rt = [](int j, int kk) constexpr {
+        int c = 0;
+        for (int r = 0; r < C::MB; ++r)
+            for (int t = 0; t < C::DEG[r]; ++t)
+                if (C::COL[r][t] == j) {
+                    if (c == kk) return r * 64 + t;
+                    ++c;
+                }
+        return -1;
+    };
+    auto vload = [&](auto jj, auto kk) __attribute__((always_inline)) {
+        constexpr int rt = col_rt(decltype(jj)::value, decltype(kk)::value), r = rt / 64, t = rt % 64;
+        if constexpr (C::SHR[r][t] == 0) return m0[rs_zero_index<C>(r, t)];
+        else return vref(std::integral_constant<int, r>{}, std::integral_constant<int, t>{});
+    };
+    auto zsum = [&](auto jj) __attribute__((always_inline)) {  // z = 0.5 * (L + ascending sum of c2v)
+        constexpr int j = decltype(jj)::value;
+        float x[col_deg<C>(j)];
+        static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) { x[kk] = vload(jj, kk); });
+        float Ssum = 0.0f;
+        static_for<0, col_deg<C>(j)>([&](auto kk) __attribute__((always_inline)) { Ssum += x[kk]; });
+        return sp_z(Lr_at(j), Ssum);
+    };
+
+    for (int it = 0; it < iters; ++it) {
+        // VN phase (variable frame): every column's c2v -> v2c as signed a, written back in place
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            constexpr int dj = col_deg<C>(j);
+            float x[dj];
+            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) { x[kk] = vload(jj, kk); });
+            const float Lj = Lr_at(j);
+            vn_excl_sums<dj, QC_RS_SERIAL>(
+                [&](auto kk) __attribute__((always_inline)) { return x[kk]; },
+                [&](auto kk, float Ssum) __attribute__((always_inline)) {
+                    x[kk] = vn_signed_a(sp_vn_arg(Lj, Ssum));  // the (D, S) form's VC output (common.h)
+                    if constexpr (QC_RS_SERIAL > 0 && (decltype(kk)::value + 1) % QC_RS_SERIAL == 0)
+                        SP_TIE("+v"(x[kk]));
+                });
+            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
+                constexpr int rt = col_rt(j, decltype(kk)::value), r = rt / 64, t = rt % 64;
+                if constexpr (C::SHR[r][t] == 0) m0[rs_zero_index<C>(r, t)] = x[kk];
+            });
+            if (live) {
+                static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
+                    constexpr int rt = col_rt(j, decltype(kk)::value), r = rt / 64, t = rt % 64;
+                    if constexpr (C::SHR[r][t] != 0)
+                        vref(std::integral_constant<int, r>{}, std::integral_constant<int, t>{}) = x[kk];
+                });
+            }
+        });
+        __syncthreads();
+        // CN phase (check frame): every row's v2c -> c2v, written back in place
+        static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value;
+            constexpr int d = C::DEG[r];
+            float g[d];
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                if constexpr (C::SHR[r][t] == 0) g[t] = m0[rs_zero_index<C>(r, t)];
+                else g[t] = cref(rr, tt);
+            });
+            cn_ds_row<d, QC_RS_SERIAL_ROW>(g, cmax2);  // O(d) exclusive sets (common.h)
+            static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                constexpr int t = decltype(tt)::value;
+                if constexpr (C::SHR[r][t] == 0) m0[rs_zero_index<C>(r, t)] = g[t];
+            });
+            if (live) {
+                static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+                    if constexpr (C::SHR[r][decltype(tt)::value] != 0) cref(rr, tt) = g[decltype(tt)::value];
+                });
+            }
+        });
+        __syncthreads();
+    }
+    if (valid) {
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
+            constexpr int j = decltype(jj)::value;
+            const float zz = zsum(jj);
+            int t = zc + C::PHI[j];
+            t -= (t >= Z) ? Z : 0;
+            const int64_t o = cw * N + j * Z + t;
+            if (bits) bits[o] = (uint8_t)Num<float>::bit(zz);
+            if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
+        });
+        if (k == 0 && l == 0 && iters_used) iters_used[cw] = iters;
+    }
+}
+
 }  // namespace ldpc

@@ -27,10 +27,13 @@ What it records (all .npz, numeric arrays only — loadable with allow_pickle=Fa
   * bp_<code>_sp.npz       802.11n (648,1/2), (1296,2/3), (1944,5/6): p1 and z, 5 iterations, clamp 10.
   * bp_<code>_sp_it<k>.npz the same at 50 / 20 / 10 iterations (one reference layer looped, checked bitwise
                            against BeliefPropagation(H, 5) first).
-  * bp_wifi648_12_sp_it50_cl20.npz  (648,1/2) 50 iterations at clamp 20, above the p-clamp ceiling.
+  * bp_wifi648_12_sp_it50_cl20.npz  (648,1/2) 50 iterations at clamp 20, above the p-clamp ceiling; plus
+                           (wificlampb32) the reference's .double() module with the fp32 module's p-clamp bound
+                           swapped in at run time (f32_pclamp): p1_f64b32_* / z_f64b32_*.
 
-    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp]   (no argument: all)
+    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32]
 """
+import contextlib
 import os
 import sys
 
@@ -348,6 +351,59 @@ def gen_wifi_sp_long(specs=None, clamp_tag=False):
                             clamp=clamp, snrs=np.array(snrs), chunk=chunk, **rec)
 
 
+@contextlib.contextmanager
+def f32_pclamp():
+    """The fp32 module's p-clamp bound in fp64 arithmetic: bp_cv.py:44-47 clamps p to +-(1 - epsilon), epsilon =
+    .0000001, and torch rounds that Python float to the tensor's dtype — 0.99999988 in the fp32 module, 0.9999999
+    in .double().  Inside this context torch.clamp called with exactly that bound on a float64 tensor uses
+    float32(1 - 1e-7) instead, so the reference's OWN fp64 module computes the fp32 module's function (messages
+    capped at log(16777215) = 16.6355 rather than log(19999999) = 16.8112).  Every other clamp — the caller's
+    x.clamp(-clamp, clamp) of bp.py:47 is the Tensor method — is untouched.  Build container only."""
+    orig = torch.clamp
+    bound = 1 - .0000001                          # the expression bp_cv.py evaluates
+    b32 = float(np.float32(bound))
+    hits = [0]
+
+    def clamp(t, *args, **kw):
+        if torch.is_tensor(t) and t.dtype == torch.float64 and args == (-bound, bound) and not kw:
+            hits[0] += 1
+            return orig(t, -b32, b32)
+        return orig(t, *args, **kw)
+    torch.clamp = clamp
+    try:
+        yield hits
+    finally:
+        torch.clamp = orig
+
+
+def gen_wifi_clamp_f32bound():
+    """Adds p1_f64b32_<tag> / z_f64b32_<tag> to bp_wifi648_12_sp_it50_cl20.npz: the reference's .double() module
+    run on the file's LLRs with the fp32 module's p-clamp bound (f32_pclamp) — the fp64 target of an fp32
+    drop-in above the ceiling, from the reference itself (tests/softparity.py f64_target)."""
+    from ldpc_amd.codes import qc_expand
+    path = os.path.join(HERE, "bp_wifi648_12_sp_it50_cl20.npz")
+    d = dict(np.load(path))
+    H = qc_expand(d["base"], int(d["Z"])).astype(np.int64)
+    iters, clamp, chunk = int(d["iters"]), float(d["clamp"]), int(d["chunk"])
+    model = BeliefPropagation(H, 1)
+    model.eval()
+    for snr in d["snrs"]:
+        tag = f"snr{snr:g}".replace(".", "p")
+        llr = d[f"llr_{tag}"]
+        ps, zs = [], []
+        with f32_pclamp() as hits:
+            for s in range(0, llr.shape[0], chunk):
+                p64, z64 = run_ref_looped(model.double(), iters, clamp, llr[s:s + chunk], double=True)
+                ps.append(p64)
+                zs.append(z64)
+        assert hits[0] == iters * len(ps), hits  # the bound was swapped in every CV layer call
+        d[f"p1_f64b32_{tag}"] = np.concatenate(ps)
+        d[f"z_f64b32_{tag}"] = np.concatenate(zs)
+        print("f32-bound fp64", tag, "|dz| vs .double() max", float(np.abs(d[f"z_f64b32_{tag}"] - d[f"z_f64_{tag}"]).max()),
+              "vs fp32 module", float(np.abs(d[f"z_f64b32_{tag}"] - d[f"z_f32_{tag}"]).max()), flush=True)
+    np.savez_compressed(path, **d)
+
+
 def gen_x0():
     """bp_x0.npz: the reference forward with NON-ZERO initial messages x (bp/bp.py:43-47), which the first
     layer consumes like any later one: (64,32) at iterations 0 / 1 / 5 and (648,1/2) at 3, clamp 10, x drawn
@@ -378,9 +434,10 @@ def gen_x0():
 
 
 if __name__ == "__main__":
-    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong", "wificlamp"]
+    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong", "wificlamp", "wificlampb32"]
     for part in parts:
         {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp, "x0": gen_x0,
          "wifilong": gen_wifi_sp_long,
-         "wificlamp": lambda: gen_wifi_sp_long(WIFI_SP_CLAMPS, clamp_tag=True)}[part]()
+         "wificlamp": lambda: gen_wifi_sp_long(WIFI_SP_CLAMPS, clamp_tag=True),
+         "wificlampb32": gen_wifi_clamp_f32bound}[part]()
     print("done")

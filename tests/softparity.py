@@ -11,18 +11,21 @@ error in the log).  So the target is the reference's fp64 output, and the rules 
     |z - z64| <= 1e-5 * max(1, |z64|) on **every** entry, no exclusions;
   - on decoding failures (oscillating / non-convergent codewords) BP's iteration map amplifies any fp32
     rounding (fp64 VN sums change nothing there: DESIGN.md §4), so fp32 cannot follow fp64 to 1e-5 after
-    tens of iterations — the reference's own fp32 is off by up to 2e-3 there.  Ours must stay within 1e-5
-    or within FAIL_FACTOR (2) times the reference's own fp32 error on the failing codewords of the same set,
-    whichever is larger; the entries where the reference's fp32 meets 1e-5 and ours does not are counted and
-    logged.  The factor: both errors are samples of the same chaotic amplification, and a set with ONE failing
-    codeword makes the envelope a single sample — measured ratios ours/reference over all goldens are 0.01-0.6
-    with several failures, 0.92 and 1.05 on the one failing codeword of the 50-iteration (648,1/2) 2 dB sets.
+    tens of iterations — the reference's own fp32 is off by up to 2e-3 there.  Asserted, per golden set:
+    (i) the maximum is within max(1e-5, the reference's own fp32 error on the failing codewords of the set);
+    (ii) the maximum and (iii) the number of entries where the reference's fp32 meets 1e-5 and ours does not
+    are at most their MEASURED values (FAILURE_BOUNDS: the GPU kernels — register, sliced and generic CSR
+    give bitwise-equal z — and the C oracle's (D, S) form, each measured; a set not listed must have none).
+    A change of the fp32 arithmetic that moves any of them fails here and must re-measure (DESIGN §4 holds
+    the trace of where the failing codewords leave the reference's fp32).
 
 A caller's clamp above the fp32 module's p-clamp ceiling log(16777215) = 16.6355 (bp_cv.py:44-47 with the bound
 1-1e-7 rounded to fp32) lets messages reach that ceiling, which the .double() module puts at log(19999999) =
 16.8112 instead: the fp32 and fp64 modules then compute different functions.  The decoder is an fp32 drop-in, so
-for such files the p1 and z targets are `f64_target`: the reference's operations in fp64 with the fp32 module's bound
-(oracle sp_f64(ceiling="f32"), equal to the .double() module wherever no message reaches either ceiling).
+for such files the p1 and z targets are `f64_target`: the REFERENCE's own .double() module run with the fp32 module's
+bound swapped in at run time (tests/golden/make_golden.py f32_pclamp: p1_f64b32_* / z_f64b32_*; the oracle's
+sp_f64(ceiling="f32") follows it to 1e-9, tests/test_oracle_golden.py), equal to the plain .double() module wherever
+no message reaches either ceiling.
 
 Each check appends its measured maxima to $LDPC_PARITY_LOG (JSON lines) when that is set; the GPU
 scripts collect them into profiles/.
@@ -33,7 +36,32 @@ import os
 import numpy as np
 
 TOL = 1e-5
-FAIL_FACTOR = 2.0
+# (kind, golden set, implementation) -> (entries where the reference's fp32 is within 1e-5 and ours is not, the
+# maximum error on decoding failures): measured (GPU: gpurun_out/r4a soft_parity.jsonl, round 4, every kernel
+# family; oracle: the CPU suite), the maxima rounded up in the third digit.  Unlisted sets: count 0.
+FAILURE_BOUNDS = {
+    ("z", "wifi648_12_sp_it50 snr1", "gpu"): (430, 1.19e-4),
+    ("p1", "wifi648_12_sp_it50 snr1", "gpu"): (35, 2.89e-5),
+    ("z", "wifi648_12_sp_it50 snr2", "gpu"): (18, 1.18e-3),
+    ("p1", "wifi648_12_sp_it50 snr2", "gpu"): (22, 2.75e-4),
+    ("z", "wifi648_12_sp_it50_cl20 snr2", "gpu"): (15, 7.21e-4),
+    ("p1", "wifi648_12_sp_it50_cl20 snr2", "gpu"): (14, 1.70e-4),
+    ("z", "wifi1296_23_sp_it20 snr2", "gpu"): (1, 1.10e-5),
+    ("z", "wifi648_12_sp_it50 snr1", "oracle"): (64, 9.24e-5),
+    ("p1", "wifi648_12_sp_it50 snr1", "oracle"): (2, 2.12e-5),
+    ("z", "wifi648_12_sp_it50 snr2", "oracle"): (17, 5.22e-4),
+    ("p1", "wifi648_12_sp_it50 snr2", "oracle"): (10, 1.23e-4),
+    ("z", "wifi648_12_sp_it50_cl20 snr2", "oracle"): (14, 3.42e-4),
+    ("p1", "wifi648_12_sp_it50_cl20 snr2", "oracle"): (9, 8.02e-5),
+}
+
+
+def _bounds(kind, label):
+    """FAILURE_BOUNDS entry of a check label ('<set> <tag> auto|generic' for the GPU, 'oracle-ds <set> <tag>')."""
+    parts = label.split()
+    impl = "oracle" if parts[0] == "oracle-ds" else "gpu"
+    key = " ".join(parts[1:3]) if impl == "oracle" else " ".join(parts[:2])
+    return FAILURE_BOUNDS.get((kind, key, impl))
 CEILING_F32 = float(np.log(np.float64(16777215.0)))  # log((1+p)/(1-p)) at p = (float)(1-1e-7)
 
 
@@ -42,9 +70,7 @@ def f64_target(d, tag, H):
     clamp = float(d["clamp"])
     if clamp <= CEILING_F32:
         return d[f"p1_f64_{tag}"], d[f"z_f64_{tag}"]
-    import oracle
-    r = oracle.sp_f64(H, d[f"llr_{tag}"].astype(np.float64), int(d["iters"]), clamp, ceiling="f32")
-    return r["p1"], r["z"]
+    return d[f"p1_f64b32_{tag}"], d[f"z_f64b32_{tag}"]   # the reference's fp64 module with the fp32 bound
 
 
 def _log(rec):
@@ -66,7 +92,6 @@ def check_p1(label, got, ref32, ref64, H, tol=TOL):
     ref_err = np.abs(ref32 - ref64)
     conv = decoded_rows(H, 0.5 - ref64)  # p1 > 0.5 <=> bit 1 <=> z < 0
     fail_env = float(ref_err[~conv].max()) if (~conv).any() else 0.0
-    tol_fail = max(tol, FAIL_FACTOR * fail_env)
     rec = {"label": label, "kind": "p1", "entries": int(err.size), "decoded_codewords": int(conv.sum()),
            "codewords": int(err.shape[0]),
            "max_abs_on_decoded": float(err[conv].max()) if conv.any() else 0.0,
@@ -78,8 +103,7 @@ def check_p1(label, got, ref32, ref64, H, tol=TOL):
     _log(rec)
     bad = int((err[conv] > tol).sum())
     assert bad == 0, f"{label}: {bad} p1 entries of decoded codewords off by > {tol}: {rec}"
-    assert rec["max_abs_on_failures"] <= tol_fail, f"{label}: p1 on decoding failures outside max({tol}, " \
-                                                   f"{FAIL_FACTOR} x the reference's own fp32 error there): {rec}"
+    _check_failures(rec, "p1", rec["max_abs_on_failures"], fail_env, "failures_entries_gt_tol_where_ref_f32_within", tol)
     return rec
 
 
@@ -98,7 +122,6 @@ def check_z(label, got, z32, z64, H):
     ref_err = np.abs(z32 - z64) / scale
     conv = decoded_rows(H, z64)
     fail_env = float(ref_err[~conv].max()) if (~conv).any() else 0.0
-    tol_fail = max(TOL, FAIL_FACTOR * fail_env)
     ref_ok = ref_err <= TOL
     rec = {"label": label, "kind": "z", "entries": int(err.size), "codewords": int(err.shape[0]),
            "decoded_codewords": int(conv.sum()),
@@ -111,6 +134,19 @@ def check_z(label, got, z32, z64, H):
     _log(rec)
     bad = int((err[conv] > TOL).sum())
     assert bad == 0, f"{label}: {bad} z entries of decoded codewords off by > {TOL} relative: {rec}"
-    assert rec["max_rel_on_failures"] <= tol_fail, f"{label}: z on decoding failures outside max(1e-5, " \
-                                                   f"{FAIL_FACTOR} x the reference's own fp32 error there): {rec}"
+    _check_failures(rec, "z", rec["max_rel_on_failures"], fail_env, "failures_entries_rel_gt_1e-5_where_ref_f32_within",
+                    TOL)
     return rec
+
+
+def _check_failures(rec, kind, got_max, ref_env, count_key, tol):
+    """The decoding-failure rules (module docstring): (i) within max(tol, the reference's own fp32 error),
+    (ii) + (iii) the maximum and the count at most their measured values."""
+    label = rec["label"]
+    assert got_max <= max(tol, ref_env), f"{label}: {kind} on decoding failures outside max({tol}, the reference's " \
+                                         f"own fp32 error there): {rec}"
+    count_m, max_m = _bounds(kind, label) or (0, max(tol, ref_env))
+    assert rec[count_key] <= count_m, f"{label}: {rec[count_key]} {kind} entries where the reference's fp32 meets " \
+                                      f"{tol} and ours does not (measured bound {count_m}): {rec}"
+    assert got_max <= max_m, f"{label}: {kind} maximum on decoding failures {got_max:.3e} above the measured " \
+                             f"{max_m:.3e}: {rec}"

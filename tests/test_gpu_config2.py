@@ -1,0 +1,80 @@
+"""BASELINE config [2] at its own iteration count: 802.11n (1944,5/6) tanh sum-product, 50 iterations, on 16-QAM
+OFDM LLRs from the on-device front end — exactly the leg bench.py times (side.configs.config2) — against the C
+oracle's (D, S)-form fp32 restatement (oracle.sp_f32(stable=True), the kernels' specification; restating
+bp_vc.py:16-27 / bp_cv.py:22-50).  The reference's own goldens for this code stop at 10 iterations
+(tests/golden/bp_wifi1944_56_sp_it10.npz, test_gpu_parity.py); its dense E x E masks make 50 iterations of the
+(1944,5/6) module a 3-4 GB-per-layer forward, so the 50-iteration soft targets are the oracle's.
+
+Tolerances: hard bits identical on every codeword the oracle decodes (zero syndrome) and z within 1e-5
+relative (scale max(1, |z|)) there; on decoding failures 50 iterations amplify ulp-level exp/log
+differences, so their count is compared, not their bits."""
+import numpy as np
+import pytest
+
+import oracle
+from softparity import _log
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+import ldpc_amd  # noqa: E402
+from ldpc_amd.channel import ofdm_demod, ofdm_tx  # noqa: E402
+from ldpc_amd.codes import Encoder, get_code  # noqa: E402
+
+TOL_Z_REL = 1e-5
+
+
+def _qam16_llrs(H, B, ebn0, seed):
+    """(codewords, LLRs) of B random codewords through 16-QAM OFDM (ofdm_size 32) at Eb/N0, as bench.py does."""
+    n = H.shape[1]
+    rate = 1 - H.shape[0] / n
+    enc = Encoder(H)
+    rng = np.random.default_rng(seed)
+    cw = enc.encode(rng.integers(0, 2, size=(B, enc.k))).astype(np.uint8)
+    s = torch.from_numpy(cw.reshape(-1)).cuda()
+    pad = (-s.numel()) % (4 * 32)
+    if pad:
+        s = torch.cat([s, torch.zeros(pad, dtype=torch.uint8, device="cuda")])
+    esn0 = float(10.0 ** (ebn0 / 10.0) * rate * 4)
+    rx = ofdm_tx(s, 32, 4, esn0, seed, 0)
+    llr = ofdm_demod(rx, 32, 4, esn0)[:B * n].view(B, n).contiguous()
+    return cw, llr
+
+
+@pytest.mark.parametrize("ebn0", [6.0, 6.5])
+def test_config2_tanh50_16qam_vs_oracle(ebn0):
+    H, _ = get_code("wifi1944_56")
+    B = 256
+    cw, x = _qam16_llrs(H, B, ebn0, seed=40 + int(ebn0 * 10))
+    dec = ldpc_amd.get_decoder(H)
+    assert dec.qc_z == 81
+    r = dec.decode(x, 50, algo="tanh", clamp=20.0, soft="z")    # bench's config [2] leg: clamp 20, 50 it
+    llr = x.cpu().numpy()
+    ref = oracle.sp_f32(H, llr, 50, 20.0, stable=True)
+    g = ldpc_amd.codes.Graph.from_H(H)
+    par = np.add.reduceat(ref["bits"][:, g.col_idx].astype(np.int64), g.row_ptr[:-1], axis=1) % 2
+    ok = ~par.any(axis=1)
+    bits = r["bits"].cpu().numpy()
+    gpar = np.add.reduceat(bits[:, g.col_idx].astype(np.int64), g.row_ptr[:-1], axis=1) % 2
+    assert ok.sum() >= B // 4, ok.sum()                      # enough decoded codewords to mean something
+    assert np.array_equal(bits[ok], ref["bits"][ok])
+    assert np.array_equal(ref["bits"][ok], cw[ok])           # and they are the transmitted codewords
+    assert abs(int((~gpar.any(axis=1)).sum()) - int(ok.sum())) <= max(1, B // 32)
+    z = r["soft"].cpu().numpy().astype(np.float64)[ok]
+    rel = np.abs(z - ref["z"][ok]) / np.maximum(1.0, np.abs(ref["z"][ok]))
+    _log({"label": f"config2 wifi1944_56 tanh 50 it 16-QAM {ebn0} dB decoded", "kind": "z_rel_vs_oracle",
+          "max": float(rel.max()), "decoded": int(ok.sum()), "of": B, "tol": TOL_Z_REL})
+    assert rel.max() <= TOL_Z_REL
+
+
+def test_config2_kernels_agree_at_50_iterations():
+    """The on-chip sliced kernel and the generic CSR kernels perform the same operations in the same order:
+    bits and z bitwise equal at config [2]'s 50 iterations on its 16-QAM LLRs (decoded and failing codewords
+    alike), including a ragged batch (odd B: the last unit's second codeword is absent)."""
+    H, _ = get_code("wifi1944_56")
+    dec = ldpc_amd.get_decoder(H)
+    for B, e in ((301, 6.0), (64, 5.5)):
+        _, x = _qam16_llrs(H, B, e, seed=7 + B)
+        a = dec.decode(x, 50, algo="tanh", clamp=20.0, soft="z")
+        b = dec.decode(x, 50, algo="tanh", clamp=20.0, soft="z", force_generic=True)
+        assert torch.equal(a["bits"], b["bits"])
+        assert torch.equal(a["soft"].view(torch.int32), b["soft"].view(torch.int32))

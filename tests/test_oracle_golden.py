@@ -179,6 +179,25 @@ def test_ceiling_golden_separates_f32_and_f64_modules():
     assert (np.abs(d["z_f32_snr3"] - t32) / np.maximum(1.0, np.abs(t32))).max() > 1e-3  # the fp32 module's own
 
 
+def test_oracle_f32_bound_f64_pinned_to_reference():
+    """Above the ceiling the soft target is the REFERENCE's own .double() module with the fp32 module's p-clamp
+    bound swapped in at run time (make_golden.py f32_pclamp -> p1_f64b32_* / z_f64b32_*): the oracle's
+    sp_f64(ceiling="f32") restates exactly that function — within fp64 rounding of the reference (<= 1e-9 in z over
+    50 iterations, decoding failures included); and that target differs from the plain .double() module by the
+    ceiling alone (> 0.1 on ceiling-bound entries)."""
+    from ldpc_amd.codes import qc_expand
+    d = np.load(os.path.join(GOLDEN, "bp_wifi648_12_sp_it50_cl20.npz"))
+    H = qc_expand(d["base"], int(d["Z"]))
+    for snr in d["snrs"]:
+        tag = f"snr{snr:g}".replace(".", "p")
+        r = oracle.sp_f64(H, d[f"llr_{tag}"].astype(np.float64), int(d["iters"]), float(d["clamp"]), ceiling="f32")
+        zb = d[f"z_f64b32_{tag}"]
+        assert np.abs(r["z"] - zb).max() <= 1e-9 * max(1.0, np.abs(zb).max())
+        assert np.abs(r["p1"] - d[f"p1_f64b32_{tag}"]).max() <= 1e-10
+        assert np.abs(zb - d[f"z_f64_{tag}"]).max() > 0.1
+        assert np.array_equal(r["bits"], np.round(d[f"p1_f64b32_{tag}"]).astype(np.uint8))
+
+
 def test_looped_reference_golden_settings():
     """The long-iteration goldens are the drop-in's / BASELINE configs' settings."""
     want = {"wifi648_12": (50, 192), "wifi1296_23": (20, 96), "wifi1944_56": (10, 48)}

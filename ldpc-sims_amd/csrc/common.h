@@ -225,10 +225,18 @@ __device__ __forceinline__ float ds_join_out(DSet p, DSet q, uint32_t sgn, float
 #ifndef DS_TSHARE
 #define DS_TSHARE 1
 #endif
-template <int d, int SERIAL>
+// LAG = 1 (with SERIAL = 1): the running prefix after edge t is tied to edge t - 1's output instead of edge t's,
+// so edge t's output (rcp, log) overlaps edge t + 1's join — two edges in flight, same operations.
+template <int t, int LAG, int d>
+__device__ __forceinline__ void ds_tie(DSet& pre, float (&g)[d]) {
+    if constexpr (LAG == 0) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+    else if constexpr (t >= LAG) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t - LAG]));
+}
+template <int d, int SERIAL, int LAG = 0>
 __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
     const float clamp = cmax2;  // (log2 units, sp_cmax2)
     constexpr auto tie_after = [](int t) { return SERIAL > 0 && (t + 1) % SERIAL == 0; };
+
     // xor of the row's sign words, three at a time (v_bitop3_b32 0x96)
     uint32_t sg = f2u(g[0]);
     static_for<0, (d - 1) / 2>([&](auto pp) __attribute__((always_inline)) {
@@ -308,7 +316,7 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
                 if constexpr (t == 0) pre = {a, 1.0f};
                 else if constexpr (t < d - 1) pre = ds_push(pre, a);
                 g[t] = y;
-                if constexpr (tie_after(t)) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+                if constexpr (tie_after(t)) ds_tie<t, LAG>(pre, g);
             });
         });
     } else {
@@ -330,7 +338,7 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
             const float y = ds_join_out(pre, {sD[t + 1], sS[t + 1]}, sg ^ f2u(g[t]), clamp);
             pre = ds_push(pre, a);
             g[t] = y;
-            if constexpr (tie_after(t)) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
+            if constexpr (tie_after(t)) ds_tie<t, LAG>(pre, g);
         });
         g[d - 1] = ds_out(pre.D, pre.S, sg ^ f2u(g[d - 1]), clamp);
     }

@@ -330,10 +330,19 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
 #define QC_RS_SERIAL_ROW 1  // the check rows' ties (cn_ds_row's SERIAL); 2: 59 VGPRs spilled
 #endif
 #ifndef QC_RS_ADDR_OPAQUE
-#define QC_RS_ADDR_OPAQUE 1  // address VGPRs passed through an empty asm at each use (a v_mov each)
+#define QC_RS_ADDR_OPAQUE 0  // 1: address VGPRs through an empty asm at each use (a v_mov each: 4.09 vs 4.28 M cw/s)
+#endif
+#ifndef QC_RS_ROW_LAG
+#define QC_RS_ROW_LAG 0  // 1: the check rows' ties lag one edge (two edges' outputs in flight, common.h)
+#endif
+#ifndef QC_RS_VPF
+#define QC_RS_VPF 0  // 1: the VN phase loads column j + 1's messages before column j's chains and stores
+#endif
+#ifndef QC_RS_CPF
+#define QC_RS_CPF 0  // k > 0: the CN phase loads the last k edges of row r + 1 (read first) before row r's chains
 #endif
 #ifndef QC_RS_L
-#define QC_RS_L 2  // where L lives: 0 VGPRs (loaded once), 2 re-read from global memory at every use
+#define QC_RS_L 0  // where L lives: 0 VGPRs (loaded once), 2 re-read from global memory at every use (3.64 vs 4.09)
 #endif
 
 template <class C>
@@ -359,6 +368,12 @@ constexpr int rs_zero_index(int r, int t) {  // index of circulant (r, t) among 
 template <class C>
 constexpr int rs_rot_total() {
     return rs_rot_index<C>(C::MB - 1, C::DEG[C::MB - 1] - 1) + (C::SHR[C::MB - 1][C::DEG[C::MB - 1] - 1] != 0);
+}
+template <class C>
+constexpr int max_col_deg() {
+    int m = 1;
+    for (int j = 0; j < C::NB; ++j) m = col_deg<C>(j) > m ? col_deg<C>(j) : m;
+    return m;
 }
 template <int Z>
 constexpr int rs_q() {  // the smallest Q with Q * Q >= Z (9 for 81)
@@ -470,11 +485,26 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
 
     for (int it = 0; it < iters; ++it) {
         // VN phase (variable frame): every column's c2v -> v2c as signed a, written back in place
+        constexpr int DV = max_col_deg<C>();
+        float xn[DV];  // QC_RS_VPF: the next column's messages, loaded one column ahead
+        if constexpr (QC_RS_VPF) {
+            static_for<0, col_deg<C>(0)>([&](auto kk) __attribute__((always_inline)) {
+                xn[kk] = vload(std::integral_constant<int, 0>{}, kk);
+            });
+        }
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             constexpr int dj = col_deg<C>(j);
             float x[dj];
-            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) { x[kk] = vload(jj, kk); });
+            static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
+                if constexpr (QC_RS_VPF) x[kk] = xn[kk];
+                else x[kk] = vload(jj, kk);
+            });
+            if constexpr (QC_RS_VPF && j + 1 < NB) {  // other slots than column j's: no hazard with its stores
+                static_for<0, col_deg<C>(j + 1)>([&](auto kk) __attribute__((always_inline)) {
+                    xn[kk] = vload(std::integral_constant<int, j + 1>{}, kk);
+                });
+            }
             const float Lj = Lr_at(j);
             vn_excl_sums<dj, QC_RS_SERIAL>(
                 [&](auto kk) __attribute__((always_inline)) { return x[kk]; },
@@ -497,6 +527,16 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
         });
         __syncthreads();
         // CN phase (check frame): every row's v2c -> c2v, written back in place
+        constexpr int KP = QC_RS_CPF > 0 ? QC_RS_CPF : 1;
+        float gn[KP];  // QC_RS_CPF: the last KP edges of the next row, loaded one row ahead
+        auto cpf = [&](auto rr) __attribute__((always_inline)) {
+            constexpr int r = decltype(rr)::value, d = C::DEG[r];
+            static_for<0, (KP < d ? KP : d)>([&](auto uu) __attribute__((always_inline)) {
+                constexpr int t = d - 1 - decltype(uu)::value;
+                if constexpr (C::SHR[r][t] != 0) gn[decltype(uu)::value] = cref(rr, std::integral_constant<int, t>{});
+            });
+        };
+        if constexpr (QC_RS_CPF > 0) cpf(std::integral_constant<int, 0>{});
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
             constexpr int r = decltype(rr)::value;
             constexpr int d = C::DEG[r];
@@ -504,9 +544,11 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 if constexpr (C::SHR[r][t] == 0) g[t] = m0[rs_zero_index<C>(r, t)];
+                else if constexpr (QC_RS_CPF > 0 && t >= d - KP) g[t] = gn[d - 1 - t];
                 else g[t] = cref(rr, tt);
             });
-            cn_ds_row<d, QC_RS_SERIAL_ROW>(g, cmax2);  // O(d) exclusive sets (common.h)
+            if constexpr (QC_RS_CPF > 0 && r + 1 < MB) cpf(std::integral_constant<int, r + 1>{});
+            cn_ds_row<d, QC_RS_SERIAL_ROW, QC_RS_ROW_LAG>(g, cmax2);  // O(d) exclusive sets (common.h)
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 if constexpr (C::SHR[r][t] == 0) m0[rs_zero_index<C>(r, t)] = g[t];

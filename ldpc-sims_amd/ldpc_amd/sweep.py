@@ -9,6 +9,9 @@ channel, LLRs, decode, then
 The channel is BPSK/AWGN generated on device (``ldpc_awgn_llr``), distributionally identical to the
 reference's QPSK over unitary-DFT OFDM at SNR(dB) = Eb/N0(dB) for rate 1/2.
 Results can be written in the reference's ``outputs/ber/*.pkl`` key schema so ``plots.py`` reads them.
+Long sweeps resume per SNR point: with ``--checkpoint`` (default ``<out>.points.jsonl`` when ``--out`` is
+given) every finished point's world-summed counters are appended as one JSON line keyed by the sweep's
+configuration, and a restarted sweep with the same configuration skips the points already recorded.
 
     python -m ldpc_amd.sweep --code peg64_32 --algo tanh --iters 3 --clamp 20 --snr 0:1:10 --n 65536
     torchrun --nproc-per-node 8 -m ldpc_amd.sweep ...        # shards codewords; one RCCL all-reduce
@@ -28,13 +31,13 @@ from .api import get_decoder
 from .codes import get_code
 from .channel import adc_quantize, ofdm_demod, ofdm_tx
 from .synth import DeviceEncoder
-from .dist import ebn0_sigma, sweep as dist_sweep
+from .dist import ebn0_sigma, shard_bounds
 
 
 def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=0.0, snr_db=(0.0,),
         codewords=65536, batch=65536, seed=1, rank=0, world=1, device=0, early_stop=False, qstep=1.0,
-        qmax=15, app_max=127, mod="bpsk", ofdm_size=32, adc_bits=None, clip_ratio=2.0):
-    """Returns dict(snrdb, uncoded_ber, coded_ber, coded_bler, codewords, seconds).
+        qmax=15, app_max=127, mod="bpsk", ofdm_size=32, adc_bits=None, clip_ratio=2.0, checkpoint=None):
+    """Returns dict(snrdb, uncoded_ber, coded_ber, coded_bler, codewords, seconds, resumed_points).
 
     ``mod``: "bpsk" (BPSK/AWGN LLRs), "qpsk-ofdm" (the reference's chain: modulate_bits, transmit_symbols,
     demodulate_signal), "16qam-ofdm" (16-QAM Gray over OFDM, exact LLRs; not in the reference).  Points
@@ -44,7 +47,12 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
     ``adc_bits`` (OFDM modes only): also run the received samples through the AGC-clipped ADC
     (``gen_qdata``, ``ofdm_functions.py:118-128``; clip = std(rx of the batch) * ``clip_ratio``) and report
     evaluate_quantized.py's ``*_quantized`` metrics and ``wmse_quantized`` (``:122``) next to the
-    unquantized ones."""
+    unquantized ones.
+
+    ``checkpoint``: a JSON-lines file of finished points (see the module docstring): points recorded there
+    for this exact configuration (every argument that shapes the data or the decode, the point's index and
+    value, the world size) are taken from it instead of being decoded again; rank 0 appends each newly
+    finished point as soon as its counters are summed over the ranks."""
     import torch
     H, _ = get_code(code) if isinstance(code, str) else (code, None)
     m, n = H.shape
@@ -102,21 +110,74 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
                 _abi.check(lib.ldpc_count_errors(bits.data_ptr(), cw.data_ptr(), B, n, k, qcnt[i].data_ptr(), st))
         return cnt.cpu().numpy()
 
-    t0 = time.perf_counter()
-    res = dist_sweep(list(snr_db), codewords, rate, k, run_shard, rank=rank, world=world, device=dev)
     from .dist import allreduce_counts
-    for t in (unc, qcnt, qunc, wmse):
+    config = dict(code=code if isinstance(code, str) else "custom", algo=algo, iters=iters,
+                  clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop, mod=mod,
+                  adc_bits=adc_bits, clip_ratio=clip_ratio if adc_bits is not None else None)
+    fp = dict(config, qstep=qstep, qmax=qmax, app_max=app_max, ofdm_size=ofdm_size, codewords=codewords,
+              batch=batch, seed=seed, world=world, snr_db=[float(x) for x in snr_db])
+    P = len(snr_db)
+    cnt = torch.zeros((P, 3), dtype=torch.int64, device=dev)
+    # points finished by an earlier run of this configuration: rank 0 reads the checkpoint, the others learn
+    # which points to skip through the same all-reduce (they contribute zeros)
+    loaded = torch.zeros((P, 1 + 3 + 1 + 3 + 1), dtype=torch.float64, device=dev)  # done, cnt, unc, qcnt, qunc, wmse
+    if checkpoint and rank == 0 and os.path.exists(checkpoint):
+        for line in open(checkpoint):
+            try:
+                rec = json.loads(line)
+            except ValueError:
+                continue  # a line cut short by an interrupted write
+            i = rec.get("i", -1)
+            if rec.get("config") == fp and 0 <= i < P and rec.get("snr") == float(snr_db[i]):
+                loaded[i] = torch.tensor([1.0, *rec["counts"], rec["uncoded"], *rec["counts_quantized"],
+                                          rec["quantized_uncoded"], rec["wmse"]], dtype=torch.float64)
+    allreduce_counts(loaded)
+    if checkpoint and rank == 0 and os.path.exists(checkpoint) and os.path.getsize(checkpoint):
+        with open(checkpoint, "rb+") as f:    # a torn last line (interrupted write): end it before appending
+            f.seek(-1, os.SEEK_END)
+            if f.read(1) != b"\n":
+                f.write(b"\n")
+    t0 = time.perf_counter()
+    resumed = []
+    for i in range(P):
+        if loaded[i, 0].item() > 0:
+            resumed.append(i)
+            if rank == 0:
+                cnt[i] = loaded[i, 1:4].to(torch.int64)
+                unc[i] = loaded[i, 4].to(torch.int64)
+                qcnt[i] = loaded[i, 5:8].to(torch.int64)
+                qunc[i] = loaded[i, 8].to(torch.int64)
+                wmse[i] = loaded[i, 9]
+            continue
+        lo, hi = shard_bounds(codewords, rank, world)
+        if hi > lo:
+            cnt[i] += torch.as_tensor(run_shard(i, lo, hi, ebn0_sigma(snr_db[i], rate)), device=dev)
+        pt = torch.cat([cnt[i].double(), unc[i:i + 1].double(), qcnt[i].double(), qunc[i:i + 1].double(),
+                        wmse[i:i + 1]])
+        allreduce_counts(pt)  # this point's counters summed over the ranks
+        if rank == 0:
+            cnt[i], unc[i], qcnt[i], qunc[i], wmse[i] = (pt[0:3].to(torch.int64), pt[3].to(torch.int64),
+                                                         pt[4:7].to(torch.int64), pt[7].to(torch.int64), pt[8])
+            if checkpoint:
+                rec = dict(config=fp, i=i, snr=float(snr_db[i]), counts=[int(v) for v in pt[0:3].tolist()],
+                           uncoded=int(pt[3].item()), counts_quantized=[int(v) for v in pt[4:7].tolist()],
+                           quantized_uncoded=int(pt[7].item()), wmse=float(pt[8].item()))
+                with open(checkpoint, "a") as f:
+                    f.write(json.dumps(rec) + "\n")
+                    f.flush()
+                    os.fsync(f.fileno())
+        else:
+            for t in (cnt[i], unc[i:i + 1], qcnt[i], qunc[i:i + 1], wmse[i:i + 1]):
+                t.zero_()  # rank 0 holds the point's totals; the closing all-reduce hands them to everyone
+    for t in (cnt, unc, qcnt, qunc, wmse):
         allreduce_counts(t)
     secs = time.perf_counter() - t0
-    c = res.counts.astype(np.float64)
+    c = cnt.cpu().numpy().astype(np.float64)
     out = dict(snrdb=np.asarray(snr_db, dtype=np.float64),
                uncoded_ber=unc.cpu().numpy() / (c[:, 2] * n),
                coded_ber=c[:, 0] / (c[:, 2] * k),
                coded_bler=c[:, 1] / c[:, 2],
-               codewords=c[:, 2].astype(np.int64), seconds=secs,
-               config=dict(code=code if isinstance(code, str) else "custom", algo=algo, iters=iters,
-                           clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop, mod=mod,
-                           adc_bits=adc_bits, clip_ratio=clip_ratio if adc_bits is not None else None))
+               codewords=c[:, 2].astype(np.int64), seconds=secs, resumed_points=resumed, config=config)
     if adc_bits is not None:
         q = qcnt.cpu().numpy().astype(np.float64)
         out.update(uncoded_ber_quantized=qunc.cpu().numpy() / (c[:, 2] * n),
@@ -191,6 +252,8 @@ def main(argv=None):
     ap.add_argument("--adc-bits", type=int, default=None, help="also decode through the AGC-clipped ADC")
     ap.add_argument("--clip-ratio", type=float, default=2.0)
     ap.add_argument("--out", default=None, help="results .json or .pkl (reference schema)")
+    ap.add_argument("--checkpoint", default=None,
+                    help="per-point resume file (JSON lines); default <out>.points.jsonl when --out is given")
     a = ap.parse_args(argv)
     import torch
     import torch.distributed as dist
@@ -208,8 +271,9 @@ def main(argv=None):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    ckpt = a.checkpoint or (a.out + ".points.jsonl" if a.out else None)
     r = run(a.code, a.algo, a.iters, a.clamp, a.alpha, a.beta, _parse_points(a.snr), a.n, a.batch, a.seed,
-            rank, world, local, a.early_stop, mod=a.mod, adc_bits=a.adc_bits, clip_ratio=a.clip_ratio)
+            rank, world, local, a.early_stop, mod=a.mod, adc_bits=a.adc_bits, clip_ratio=a.clip_ratio, checkpoint=ckpt)
     if rank == 0:
         for i, e in enumerate(r["snrdb"]):
             line = (f"{e:5.2f} dB  uncoded {r['uncoded_ber'][i]:.4e}  coded BER {r['coded_ber'][i]:.4e}  "
@@ -218,7 +282,7 @@ def main(argv=None):
                 line += (f" | ADC uncoded {r['uncoded_ber_quantized'][i]:.4e} BER {r['coded_ber_quantized'][i]:.4e} "
                          f"BLER {r['coded_bler_quantized'][i]:.4e} wmse {r['wmse_quantized'][i]:.4g}")
             print(line)
-        print(f"{r['seconds']:.2f} s")
+        print(f"{r['seconds']:.2f} s" + (f" (points {r['resumed_points']} from {ckpt})" if r["resumed_points"] else ""))
         if a.out:
             save(r, a.out)
     if world > 1:

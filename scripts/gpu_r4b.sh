@@ -1,8 +1,10 @@
 #!/bin/bash
-# Round 4 session b: config [2] kernel A/B, the config [2] 50-iteration parity test, the GPU soft-output trace.
+# Round 4 session b: config [2] kernel A/B, the full GPU suite (config [2] 50-iteration parity, sweep resume, soft
+# parity with the measured failure bounds), the GPU soft-output trace.
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r4b
-VARIANTS="rsA rsAb10 rsAs2 rsAns rsAs2b10" OUT=gpurun_out/r4b bash scripts/ab_rs.sh || exit 1
-timeout -k 10 300 python -u -m pytest tests/test_gpu_config2.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r4b/pytest_c2.log 2>&1; tail -6 gpurun_out/r4b/pytest_c2.log
+VARIANTS="rsA rsAb10 rsAs2 rsV rsC8 rsLag rsVLag" OUT=gpurun_out/r4b bash scripts/ab_rs.sh || exit 1
+LDPC_PARITY_LOG=gpurun_out/r4b/soft_parity.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r4b/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/r4b/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/r4b/pytest_gpu.log
 timeout -k 10 300 python scripts/trace_failure_gpu.py

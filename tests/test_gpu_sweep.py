@@ -123,3 +123,27 @@ def test_ber_overlay_in_db():
                   "bound_db": tol, "codewords_gpu": n, "codewords_published": N})
     for kind, lv, off, sig, tol in rows:
         assert off is not None and abs(off) <= tol, (kind, lv, off, tol)
+
+
+def test_sweep_resumes_per_point(tmp_path):
+    """SURVEY §5 checkpoint/resume: every finished SNR point is appended to the checkpoint (world-summed
+    counters keyed by the configuration); a restarted sweep skips the recorded points and gives the same
+    curve as an uninterrupted one.  A record of another configuration (here: another seed) is ignored, and a
+    torn last line (an interrupted write) is skipped."""
+    import json
+    ck = str(tmp_path / "pts.jsonl")
+    args = dict(snr_db=[1.0, 2.0, 3.0], codewords=3000, batch=1024, seed=5)
+    full = run("wifi648_12", "minsum", 10, 20.0, checkpoint=ck, **args)
+    recs = [json.loads(x) for x in open(ck)]
+    assert [r["i"] for r in recs] == [0, 1, 2] and full["resumed_points"] == []
+    with open(ck, "w") as f:                      # interrupted after point 1: keep 0 and 1, a torn line after them
+        for r in recs[:2]:
+            f.write(json.dumps(r) + "\n")
+        other = dict(recs[2], config=dict(recs[2]["config"], seed=6))
+        f.write(json.dumps(other) + "\n")
+        f.write(json.dumps(recs[2])[:40])
+    again = run("wifi648_12", "minsum", 10, 20.0, checkpoint=ck, **args)
+    assert again["resumed_points"] == [0, 1]
+    for key in ("uncoded_ber", "coded_ber", "coded_bler", "codewords"):
+        assert np.array_equal(np.asarray(again[key]), np.asarray(full[key])), key
+    assert 0 < full["coded_bler"][0] < 1

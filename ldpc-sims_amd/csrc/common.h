@@ -232,7 +232,7 @@ __device__ __forceinline__ void ds_tie(DSet& pre, float (&g)[d]) {
     if constexpr (LAG == 0) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
     else if constexpr (t >= LAG) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t - LAG]));
 }
-template <int d, int SERIAL, int LAG = 0>
+template <int d, int SERIAL, int LAG = 0, int BLOCK = DS_BLOCK>
 __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
     const float clamp = cmax2;  // (log2 units, sp_cmax2)
     constexpr auto tie_after = [](int t) { return SERIAL > 0 && (t + 1) % SERIAL == 0; };
@@ -253,7 +253,7 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
         // pushes in the same order as the unblocked pass, so the outputs are bitwise the unblocked ones; the
         // cost is the T passes.  (Each block's T pushes copies of the inputs through an empty asm: otherwise
         // the compiler CSEs the passes and keeps every suffix set live, which is what blocking avoids.)
-        constexpr int BS = DS_BLOCK < d ? DS_BLOCK : d, NBK = (d + BS - 1) / BS;
+        constexpr int BS = BLOCK < d ? BLOCK : d, NBK = (d + BS - 1) / BS;
         DSet pre = {0.0f, 1.0f};
         // DS_TSHARE: one pass from the row's end yields every block's T (the sets at the block boundaries,
         // the same pushes in the same order), instead of a fresh pass per block

@@ -332,6 +332,12 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
 #ifndef QC_RS_ADDR_OPAQUE
 #define QC_RS_ADDR_OPAQUE 0  // 1: address VGPRs through an empty asm at each use (a v_mov each: 4.09 vs 4.28 M cw/s)
 #endif
+#ifndef QC_RS_DS_BLOCK
+#define QC_RS_DS_BLOCK 10  // check rows of d = 20 in two blocks (common.h cn_ds_row): 4.27 -> 4.33 M cw/s (7: 3 blocks)
+#endif
+#ifndef QC_RS_IDLE_DUP
+#define QC_RS_IDLE_DUP 0  // 1: idle lanes l >= 27 shadow lane l - 27 (same loads, same values) and store too: no exec branches
+#endif
 #ifndef QC_RS_ROW_LAG
 #define QC_RS_ROW_LAG 0  // 1: the check rows' ties lag one edge (two edges' outputs in flight, common.h)
 #endif
@@ -370,7 +376,7 @@ constexpr int rs_rot_total() {
     return rs_rot_index<C>(C::MB - 1, C::DEG[C::MB - 1] - 1) + (C::SHR[C::MB - 1][C::DEG[C::MB - 1] - 1] != 0);
 }
 template <class C>
-constexpr int max_col_deg() {
+constexpr int rs_max_col_deg() {
     int m = 1;
     for (int j = 0; j < C::NB; ++j) m = col_deg<C>(j) > m ? col_deg<C>(j) : m;
     return m;
@@ -399,8 +405,11 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
     const int64_t cw = (int64_t)blockIdx.x * 2 + h;
     const bool live = l < ZL;                // lane carries a frame position (stores are live lanes only)
     const bool valid = live && cw < B;
-    // idle lanes read at their wave's first position (a broadcast, see k_qc_sp_sl) and never store
-    const int zc = live ? l + ZL * k : ZL * k;
+    // idle lanes read at their wave's first position (a broadcast, see k_qc_sp_sl) and never store; with
+    // QC_RS_IDLE_DUP they shadow lane l - ZL instead — the same loads, so the same values, written to the same
+    // slots by the same instruction — and the stores need no exec mask
+    const int zc = live ? l + ZL * k : (QC_RS_IDLE_DUP ? l - ZL + ZL * k : ZL * k);
+    const bool store = QC_RS_IDLE_DUP ? true : live;
     // byte addresses of this lane's slot for a = 0 .. NA-1 (check side) and b = 0 .. Q-1 (variable side)
     int aC[NA], aV[Q];
 #pragma unroll
@@ -429,14 +438,15 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
         return *reinterpret_cast<float*>(Xb + a + rs_rot_index<C>(r, t) * CROW);
     };
     // L = -llr (bp.py:47) of this lane's variable in block column j: in VGPRs, or re-read at every use (L2)
-    const float* const lp = llr + (valid ? cw * N : 0);
+    const bool lval = QC_RS_IDLE_DUP ? cw < B : valid;  // shadow lanes load their partner's L
+    const float* const lp = llr + (lval ? cw * N : 0);
     float Lreg[QC_RS_L == 0 ? NB : 1];
     auto Lload = [&](int j, bool opaque) __attribute__((always_inline)) {
         int z = zc;
         if (opaque) asm volatile("" : "+v"(z));
         int t = z + C::PHI[j];
         t -= (t >= Z) ? Z : 0;
-        return valid ? -lp[j * Z + t] : 0.0f;
+        return lval ? -lp[j * Z + t] : 0.0f;
     };
     if constexpr (QC_RS_L == 0) {
 #pragma unroll
@@ -485,7 +495,7 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
 
     for (int it = 0; it < iters; ++it) {
         // VN phase (variable frame): every column's c2v -> v2c as signed a, written back in place
-        constexpr int DV = max_col_deg<C>();
+        constexpr int DV = rs_max_col_deg<C>();
         float xn[DV];  // QC_RS_VPF: the next column's messages, loaded one column ahead
         if constexpr (QC_RS_VPF) {
             static_for<0, col_deg<C>(0)>([&](auto kk) __attribute__((always_inline)) {
@@ -517,7 +527,7 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 constexpr int rt = col_rt(j, decltype(kk)::value), r = rt / 64, t = rt % 64;
                 if constexpr (C::SHR[r][t] == 0) m0[rs_zero_index<C>(r, t)] = x[kk];
             });
-            if (live) {
+            if (store) {
                 static_for<0, dj>([&](auto kk) __attribute__((always_inline)) {
                     constexpr int rt = col_rt(j, decltype(kk)::value), r = rt / 64, t = rt % 64;
                     if constexpr (C::SHR[r][t] != 0)
@@ -548,12 +558,12 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 else g[t] = cref(rr, tt);
             });
             if constexpr (QC_RS_CPF > 0 && r + 1 < MB) cpf(std::integral_constant<int, r + 1>{});
-            cn_ds_row<d, QC_RS_SERIAL_ROW, QC_RS_ROW_LAG>(g, cmax2);  // O(d) exclusive sets (common.h)
+            cn_ds_row<d, QC_RS_SERIAL_ROW, QC_RS_ROW_LAG, QC_RS_DS_BLOCK>(g, cmax2);  // O(d) exclusive sets (common.h)
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 if constexpr (C::SHR[r][t] == 0) m0[rs_zero_index<C>(r, t)] = g[t];
             });
-            if (live) {
+            if (store) {
                 static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                     if constexpr (C::SHR[r][decltype(tt)::value] != 0) cref(rr, tt) = g[decltype(tt)::value];
                 });

@@ -114,14 +114,21 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
     config = dict(code=code if isinstance(code, str) else "custom", algo=algo, iters=iters,
                   clamp=clamp, alpha=alpha, beta=beta, early_stop=early_stop, mod=mod,
                   adc_bits=adc_bits, clip_ratio=clip_ratio if adc_bits is not None else None)
+    import torch.distributed as dist
+    # counters summed over ranks only inside a process group; without one (tests: rank/world given by hand)
+    # each rank keeps its own shard's counts, and its checkpoint records are its own (rank in the key)
+    reduced = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
     fp = dict(config, qstep=qstep, qmax=qmax, app_max=app_max, ofdm_size=ofdm_size, codewords=codewords,
               batch=batch, seed=seed, world=world, snr_db=[float(x) for x in snr_db])
+    if not reduced and world > 1:
+        fp["rank"] = rank
     P = len(snr_db)
     cnt = torch.zeros((P, 3), dtype=torch.int64, device=dev)
     # points finished by an earlier run of this configuration: rank 0 reads the checkpoint, the others learn
     # which points to skip through the same all-reduce (they contribute zeros)
-    loaded = torch.zeros((P, 1 + 3 + 1 + 3 + 1), dtype=torch.float64, device=dev)  # done, cnt, unc, qcnt, qunc, wmse
-    if checkpoint and rank == 0 and os.path.exists(checkpoint):
+    loaded = torch.zeros((P, 1 + 3 + 1 + 3 + 1 + 1), dtype=torch.float64, device=dev)  # done, cnt, unc, qcnt, qunc, wmse
+    writer = rank == 0 or not reduced
+    if checkpoint and writer and os.path.exists(checkpoint):
         for line in open(checkpoint):
             try:
                 rec = json.loads(line)
@@ -132,7 +139,7 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
                 loaded[i] = torch.tensor([1.0, *rec["counts"], rec["uncoded"], *rec["counts_quantized"],
                                           rec["quantized_uncoded"], rec["wmse"]], dtype=torch.float64)
     allreduce_counts(loaded)
-    if checkpoint and rank == 0 and os.path.exists(checkpoint) and os.path.getsize(checkpoint):
+    if checkpoint and writer and os.path.exists(checkpoint) and os.path.getsize(checkpoint):
         with open(checkpoint, "rb+") as f:    # a torn last line (interrupted write): end it before appending
             f.seek(-1, os.SEEK_END)
             if f.read(1) != b"\n":
@@ -142,7 +149,7 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
     for i in range(P):
         if loaded[i, 0].item() > 0:
             resumed.append(i)
-            if rank == 0:
+            if writer:
                 cnt[i] = loaded[i, 1:4].to(torch.int64)
                 unc[i] = loaded[i, 4].to(torch.int64)
                 qcnt[i] = loaded[i, 5:8].to(torch.int64)
@@ -155,7 +162,7 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
         pt = torch.cat([cnt[i].double(), unc[i:i + 1].double(), qcnt[i].double(), qunc[i:i + 1].double(),
                         wmse[i:i + 1]])
         allreduce_counts(pt)  # this point's counters summed over the ranks
-        if rank == 0:
+        if writer:
             cnt[i], unc[i], qcnt[i], qunc[i], wmse[i] = (pt[0:3].to(torch.int64), pt[3].to(torch.int64),
                                                          pt[4:7].to(torch.int64), pt[7].to(torch.int64), pt[8])
             if checkpoint:
@@ -169,8 +176,9 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
         else:
             for t in (cnt[i], unc[i:i + 1], qcnt[i], qunc[i:i + 1], wmse[i:i + 1]):
                 t.zero_()  # rank 0 holds the point's totals; the closing all-reduce hands them to everyone
-    for t in (cnt, unc, qcnt, qunc, wmse):
-        allreduce_counts(t)
+    if reduced:
+        for t in (cnt, unc, qcnt, qunc, wmse):
+            allreduce_counts(t)
     secs = time.perf_counter() - t0
     c = cnt.cpu().numpy().astype(np.float64)
     out = dict(snrdb=np.asarray(snr_db, dtype=np.float64),

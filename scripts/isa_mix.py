@@ -4,7 +4,7 @@ objects (scripts/kernel_resources.py's bundle walk), find the kernel whose symbo
 longest backward branch's body (the iteration loop) and count its instructions by class — VALU,
 transcendental VALU (quarter rate), LDS, waitcnt, nop (hazard wait states), SALU, barriers.
 
-    python scripts/isa_mix.py LIB.so SUBSTR [--top N]
+    python scripts/isa_mix.py LIB.so SUBSTR [--top N] [--phases]
 """
 import collections
 import os
@@ -92,6 +92,13 @@ def main():
     print("  loop instructions:", len(loop), c, "nop wait states:", nops)
     if top:
         print("  ", collections.Counter(op for _, op, _, _ in loop).most_common(top))
+    if "--phases" in sys.argv:  # the loop split at its s_barrier instructions
+        bars = [i for i, (_, op, _, _) in enumerate(loop) if op == "s_barrier"] + [len(loop)]
+        lo = 0
+        for b in bars:
+            if b > lo:
+                print("   phase", mix(loop[lo:b]))
+            lo = b
 
 
 if __name__ == "__main__":

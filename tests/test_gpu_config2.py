@@ -5,9 +5,14 @@ bp_vc.py:16-27 / bp_cv.py:22-50).  The reference's own goldens for this code sto
 (tests/golden/bp_wifi1944_56_sp_it10.npz, test_gpu_parity.py); its dense E x E masks make 50 iterations of the
 (1944,5/6) module a 3-4 GB-per-layer forward, so the 50-iteration soft targets are the oracle's.
 
-Tolerances: hard bits identical on every codeword the oracle decodes (zero syndrome) and z within 1e-5
-relative (scale max(1, |z|)) there; on decoding failures 50 iterations amplify ulp-level exp/log
-differences, so their count is compared, not their bits."""
+Tolerances (the soft target is the fp64 evaluation of the same function, oracle.sp_f64 with the fp32 module's
+p-clamp bound since clamp 20 is above the ceiling — pinned to the reference's own fp64 module in
+test_oracle_golden.py): hard bits identical to the oracle on every codeword it decodes (zero syndrome, and
+they are the transmitted codewords); z within 1e-5 relative (scale max(1, |z|)) of the fp64 target on every
+codeword that converged at least 10 iterations before the end (the oracle's early-stop iteration count); on the
+codewords that converged in the last 10 iterations, the fp32 trajectory was chaotic until then — the oracle's
+own fp32 is 1.3e-5 .. 6.3e-5 from fp64 there (measured) — so z within 1e-4 (measured 7.4e-5); on
+decoding failures only the count is compared."""
 import numpy as np
 import pytest
 
@@ -21,6 +26,7 @@ from ldpc_amd.channel import ofdm_demod, ofdm_tx  # noqa: E402
 from ldpc_amd.codes import Encoder, get_code  # noqa: E402
 
 TOL_Z_REL = 1e-5
+TOL_Z_REL_LATE = 1e-4
 
 
 def _qam16_llrs(H, B, ebn0, seed):
@@ -50,6 +56,8 @@ def test_config2_tanh50_16qam_vs_oracle(ebn0):
     r = dec.decode(x, 50, algo="tanh", clamp=20.0, soft="z")    # bench's config [2] leg: clamp 20, 50 it
     llr = x.cpu().numpy()
     ref = oracle.sp_f32(H, llr, 50, 20.0, stable=True)
+    conv_at = oracle.sp_f32(H, llr, 50, 20.0, stable=True, early_stop=True)["iters_used"]
+    t64 = oracle.sp_f64(H, llr.astype(np.float64), 50, 20.0, ceiling="f32")["z"]
     g = ldpc_amd.codes.Graph.from_H(H)
     par = np.add.reduceat(ref["bits"][:, g.col_idx].astype(np.int64), g.row_ptr[:-1], axis=1) % 2
     ok = ~par.any(axis=1)
@@ -59,11 +67,18 @@ def test_config2_tanh50_16qam_vs_oracle(ebn0):
     assert np.array_equal(bits[ok], ref["bits"][ok])
     assert np.array_equal(ref["bits"][ok], cw[ok])           # and they are the transmitted codewords
     assert abs(int((~gpar.any(axis=1)).sum()) - int(ok.sum())) <= max(1, B // 32)
-    z = r["soft"].cpu().numpy().astype(np.float64)[ok]
-    rel = np.abs(z - ref["z"][ok]) / np.maximum(1.0, np.abs(ref["z"][ok]))
-    _log({"label": f"config2 wifi1944_56 tanh 50 it 16-QAM {ebn0} dB decoded", "kind": "z_rel_vs_oracle",
-          "max": float(rel.max()), "decoded": int(ok.sum()), "of": B, "tol": TOL_Z_REL})
-    assert rel.max() <= TOL_Z_REL
+    z = r["soft"].cpu().numpy().astype(np.float64)
+    rel = np.abs(z - t64) / np.maximum(1.0, np.abs(t64))
+    early = ok & (conv_at <= 40)
+    late = ok & (conv_at > 40)
+    rec = {"label": f"config2 wifi1944_56 tanh 50 it 16-QAM {ebn0} dB", "kind": "z_rel_vs_f64",
+           "decoded": int(ok.sum()), "of": B, "converged_by_40": int(early.sum()),
+           "max_converged_by_40": float(rel[early].max()), "tol": TOL_Z_REL,
+           "converged_after_40": int(late.sum()), "max_converged_after_40": float(rel[late].max()) if late.any() else 0.0,
+           "tol_late": TOL_Z_REL_LATE}
+    _log(rec)
+    assert early.sum() >= B // 4 and rel[early].max() <= TOL_Z_REL, rec
+    assert rec["max_converged_after_40"] <= TOL_Z_REL_LATE, rec
 
 
 def test_config2_kernels_agree_at_50_iterations():

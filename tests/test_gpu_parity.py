@@ -67,6 +67,12 @@ def test_decode_bits_dropin_matches_reference_golden():
     assert np.array_equal(out, d["out"])
     with pytest.raises(ZeroDivisionError):
         ldpc_amd.decode_bits(d["llrs"], d["H"], 5, 0, 10)
+    # the recycled-buffer result vs the opt-out: same values, a fresh self-owning array
+    fresh = ldpc_amd.decode_bits(d["llrs"], d["H"], int(d["iters"]), int(d["batch_size"]), int(d["clamp"]),
+                                 fresh_output=True)
+    assert fresh.flags.owndata and not out.flags.owndata
+    assert np.array_equal(fresh, d["out"]) and fresh.dtype == np.float64
+    fresh.resize((fresh.shape[0] * fresh.shape[1],), refcheck=False)   # a plain numpy array: resizable
 
 
 @pytest.mark.parametrize("chunk", [7, 48, 1000])

@@ -77,6 +77,12 @@ __device__ __forceinline__ bool tile_slot(int nodes, int tpl2, int64_t B, int& n
 #ifndef GEN_NT_LOAD
 #define GEN_NT_LOAD 0
 #endif
+// GEN_SKIP_DUP: the min-sum kernels load only the d < MAXD edges a node has (d is wave-uniform: a scalar
+// branch per slot) instead of re-loading the last edge into the unused slots (cache hits, but TA / L2 requests:
+// DVB-S2's variables have degree 8, 3 or 2 under MAXD = 8)
+#ifndef GEN_SKIP_DUP
+#define GEN_SKIP_DUP 0
+#endif
 #ifndef GEN_NT_STORE
 #define GEN_NT_STORE 0
 #endif
@@ -444,6 +450,7 @@ __global__ __launch_bounds__(256) void k_vn_ms(const int32_t* __restrict__ var_p
 #pragma unroll
     for (int k = 0; k < MAXD; ++k) {
         off[k] = (int64_t)var_edges[a + (k < d ? k : d - 1)] * ldb + cw;
+        if (GEN_SKIP_DUP && k >= d) continue;  // d is wave-uniform: a scalar branch, the loop stays unrolled
         if (first) {
 #pragma unroll
             for (int i = 0; i < V; ++i) x[k].x[i] = 0.0f;
@@ -485,7 +492,10 @@ __global__ __launch_bounds__(256) void k_cn_ms(const int32_t* __restrict__ row_p
     if (d == 0) return;
     Vec<float, V> t[MAXD];
 #pragma unroll
-    for (int k = 0; k < MAXD; ++k) t[k] = vload<float, V>(v2c + (int64_t)(a + (k < d ? k : d - 1)) * ldb + cw);
+    for (int k = 0; k < MAXD; ++k) {
+        if (GEN_SKIP_DUP && k >= d) continue;  // d is wave-uniform: a scalar branch, the loop stays unrolled
+        t[k] = vload<float, V>(v2c + (int64_t)(a + (k < d ? k : d - 1)) * ldb + cw);
+    }
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         float min1 = __builtin_inff(), min2 = __builtin_inff();

@@ -598,6 +598,20 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_ADDR_MIN_USES_EARLY
 #define QC_PH_ADDR_MIN_USES_EARLY QC_PH_ADDR_MIN_USES
 #endif
+// Phase priorities (s_setprio, round 4): a SIMD issues from the higher-priority waves first, so raising the phase
+// whose waves stall on their own dependences lets their instructions issue the moment they are ready while the
+// other phase's independent work fills the gaps.  A/B profiles/r04/ab/ab_prio.txt.
+#ifndef QC_PH_PRIO
+// phased min-sum, fixed count: 2 = s_setprio 1 over the CN phase (the rotations' gathers and the two-minimum
+// chains), 0 over the VN phase: 42.0 -> 43.4-44.0 M cw/s; 1 = the reverse (-0.7 %); 3 = 2 with the VN phase's
+// first lookahead rotations still at 1
+#define QC_PH_PRIO 2
+#endif
+#ifndef QC_SP_PRIO
+// tanh-SP register kernel, fixed count: 2 = s_setprio 1 over the VN phase (exp chains), 0 over the rows: 16.2 ->
+// 16.6 M cw/s; 1 = priority over each row's gather only (neutral)
+#define QC_SP_PRIO 2
+#endif
 #ifndef QC_PH_LA
 #define QC_PH_LA 1  // rotations issued this many rows / columns ahead, in place: +2.5 % (A/B 38.9 vs 38.0 M cw/s; 2: +2.0 %, 3: +1.5 %; 0: the plain phased order)
 #endif
@@ -935,8 +949,13 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #endif
 #if QC_PH_LA
         if constexpr (!EARLY) {
+            if constexpr (QC_PH_PRIO == 2 || QC_PH_PRIO == 3) __builtin_amdgcn_s_setprio(1);
+            if constexpr (QC_PH_PRIO == 1) __builtin_amdgcn_s_setprio(0);
             cn_phase_la();
+            if constexpr (QC_PH_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+            if constexpr (QC_PH_PRIO == 2) __builtin_amdgcn_s_setprio(0);
             static_for<0, (QC_PH_LA < NB ? QC_PH_LA : NB)>([&](auto pp) __attribute__((always_inline)) { rot_col(pp); });
+            if constexpr (QC_PH_PRIO == 3) __builtin_amdgcn_s_setprio(0);
             static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
                 constexpr int p = decltype(pp)::value;
                 if constexpr (p + QC_PH_LA < NB) rot_col(std::integral_constant<int, p + QC_PH_LA>{});
@@ -1265,6 +1284,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
             }
         }
         // VC + tanh in the variable frame: c2v -> v2c in place
+        if constexpr (!EARLY && QC_SP_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         // L of column j + LPF is loaded before column j's chain (its address asm precedes the chain's ties),
         // so its LDS latency hides under the chains instead of a lgkmcnt(0) wait per column
         constexpr int LPF = EARLY ? QC_SP_LPF_EARLY : QC_SP_LPF;
@@ -1295,6 +1315,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 });
         });
         // CV in the check frame: gather v2c, exclusive products, log, clamp, scatter c2v back
+        if constexpr (!EARLY && QC_SP_PRIO == 2) __builtin_amdgcn_s_setprio(0);
 #if QC_SP_GLA
         // gathers issued one row ahead, in place on msg[] (as k_qc_ms_ph's lookahead): row r + 1's rotations
         // are in flight while row r's chains run
@@ -1319,6 +1340,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
 #else
             constexpr bool GLA = false;
 #endif
+            if constexpr (!EARLY && QC_SP_PRIO == 1) __builtin_amdgcn_s_setprio(1);
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int s = C::SHR[r][t];
@@ -1328,6 +1350,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                     g[t] = xfer(raddr(std::integral_constant<int, s>{}), msg[e0 + t]);
                 }
             });
+            if constexpr (!EARLY && QC_SP_PRIO == 1) __builtin_amdgcn_s_setprio(0);
             cn_ds_row<d, (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32))) ? QC_SP_SERIAL_STRIDE : 0>(g, cmax2);
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;

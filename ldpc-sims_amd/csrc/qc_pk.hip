@@ -52,6 +52,11 @@ namespace ldpc {
 #ifndef QC_PK_ES_ROWS
 #define QC_PK_ES_ROWS 1  // early-stop syndrome row by row with an early exit (one codeword pair per wave, Z = 54)
 #endif
+#ifndef QC_PK_PRIO
+// 1: s_setprio 1 over the VN phase (0 over the CN phase), early stop and fixed count: config [3] 66.9 -> 67.5 M
+// cw/s (A/B profiles/r04/ab/ab_prio.txt); 2: the reverse (-1.3 %)
+#define QC_PK_PRIO 1
+#endif
 #ifndef QC_PK_TPB
 #define QC_PK_TPB 256
 #endif
@@ -286,7 +291,11 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
 
     int it = 0;
     for (; it + 1 < iters; ++it) {
+        if constexpr (QC_PK_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+        if constexpr (QC_PK_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         cn_phase();
+        if constexpr (QC_PK_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+        if constexpr (QC_PK_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         if constexpr (EARLY) {
             uint32_t app[NB];
             static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {

@@ -335,6 +335,12 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
 #ifndef QC_RS_DS_BLOCK
 #define QC_RS_DS_BLOCK 10  // check rows of d = 20 in two blocks (common.h cn_ds_row): 4.27 -> 4.33 M cw/s (7: 3 blocks)
 #endif
+#ifndef QC_RS_PRIO
+// 1: s_setprio 1 over the latency-bound VN phase (short chains between LDS loads), 0 over the issue-bound CN phase,
+// so a SIMD issues the VN waves' loads as soon as they are ready and fills the gaps with CN work: 4.35 -> 4.67 M
+// cw/s (A/B profiles/r04/ab/ab_rs.txt); 2: the reverse, 4.25; 3: as 1, and the CN phase's row gathers at 1 too
+#define QC_RS_PRIO 1
+#endif
 #ifndef QC_RS_IDLE_DUP
 #define QC_RS_IDLE_DUP 0  // 1: idle lanes l >= 27 shadow lane l - 27 (same loads, same values) and store too: no exec branches
 #endif
@@ -495,6 +501,9 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
 
     for (int it = 0; it < iters; ++it) {
         // VN phase (variable frame): every column's c2v -> v2c as signed a, written back in place
+        if constexpr (QC_RS_PRIO == 1 || QC_RS_PRIO == 3) __builtin_amdgcn_s_setprio(1);
+        if constexpr (QC_RS_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+        if constexpr (QC_RS_PRIO == 4) __builtin_amdgcn_s_setprio(3);
         constexpr int DV = rs_max_col_deg<C>();
         float xn[DV];  // QC_RS_VPF: the next column's messages, loaded one column ahead
         if constexpr (QC_RS_VPF) {
@@ -537,6 +546,8 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
         });
         __syncthreads();
         // CN phase (check frame): every row's v2c -> c2v, written back in place
+        if constexpr (QC_RS_PRIO == 1 || QC_RS_PRIO == 3 || QC_RS_PRIO == 4) __builtin_amdgcn_s_setprio(0);
+        if constexpr (QC_RS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
         constexpr int KP = QC_RS_CPF > 0 ? QC_RS_CPF : 1;
         float gn[KP];  // QC_RS_CPF: the last KP edges of the next row, loaded one row ahead
         auto cpf = [&](auto rr) __attribute__((always_inline)) {
@@ -550,6 +561,7 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
             constexpr int r = decltype(rr)::value;
             constexpr int d = C::DEG[r];
+            if constexpr (QC_RS_PRIO == 3) __builtin_amdgcn_s_setprio(1);
             float g[d];
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
@@ -557,6 +569,7 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 else if constexpr (QC_RS_CPF > 0 && t >= d - KP) g[t] = gn[d - 1 - t];
                 else g[t] = cref(rr, tt);
             });
+            if constexpr (QC_RS_PRIO == 3) __builtin_amdgcn_s_setprio(0);
             if constexpr (QC_RS_CPF > 0 && r + 1 < MB) cpf(std::integral_constant<int, r + 1>{});
             cn_ds_row<d, QC_RS_SERIAL_ROW, QC_RS_ROW_LAG, QC_RS_DS_BLOCK>(g, cmax2);  // O(d) exclusive sets (common.h)
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {

@@ -813,7 +813,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         static_for<0, (QC_PH_LA < MB ? QC_PH_LA : MB)>([&](auto rr) __attribute__((always_inline)) { gather_row(rr); });
         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
             constexpr int r = decltype(rr)::value;
+            if constexpr (!EARLY && QC_PH_PRIO == 6) __builtin_amdgcn_s_setprio(1);
             if constexpr (r + QC_PH_LA < MB) gather_row(std::integral_constant<int, r + QC_PH_LA>{});
+            if constexpr (!EARLY && QC_PH_PRIO == 6) __builtin_amdgcn_s_setprio(0);
             math_row(rr);
         });
     };
@@ -949,16 +951,18 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #endif
 #if QC_PH_LA
         if constexpr (!EARLY) {
-            if constexpr (QC_PH_PRIO == 2 || QC_PH_PRIO == 3) __builtin_amdgcn_s_setprio(1);
+            if constexpr (QC_PH_PRIO == 2 || QC_PH_PRIO == 3 || QC_PH_PRIO == 5) __builtin_amdgcn_s_setprio(1);
             if constexpr (QC_PH_PRIO == 1) __builtin_amdgcn_s_setprio(0);
             cn_phase_la();
             if constexpr (QC_PH_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-            if constexpr (QC_PH_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+            if constexpr (QC_PH_PRIO == 2 || QC_PH_PRIO == 5) __builtin_amdgcn_s_setprio(0);
             static_for<0, (QC_PH_LA < NB ? QC_PH_LA : NB)>([&](auto pp) __attribute__((always_inline)) { rot_col(pp); });
             if constexpr (QC_PH_PRIO == 3) __builtin_amdgcn_s_setprio(0);
             static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
                 constexpr int p = decltype(pp)::value;
+                if constexpr (QC_PH_PRIO == 5) __builtin_amdgcn_s_setprio(1);
                 if constexpr (p + QC_PH_LA < NB) rot_col(std::integral_constant<int, p + QC_PH_LA>{});
+                if constexpr (QC_PH_PRIO == 5) __builtin_amdgcn_s_setprio(0);
                 v2c_col(std::integral_constant<int, lcol<C>(p)>{}, sum_col(pp));
             });
             continue;

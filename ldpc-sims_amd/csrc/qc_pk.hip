@@ -52,6 +52,11 @@ namespace ldpc {
 #ifndef QC_PK_ES_ROWS
 #define QC_PK_ES_ROWS 1  // early-stop syndrome row by row with an early exit (one codeword pair per wave, Z = 54)
 #endif
+#ifndef QC_PK_DIAG
+// DIAGNOSTIC BUILDS ONLY (wrong results; DESIGN.md §3.3, scripts/pk_floor_diag.sh): 1 = no bit stores, 2 = no
+// LLR loads — prices the per-launch data movement
+#define QC_PK_DIAG 0
+#endif
 #ifndef QC_PK_PRIO
 // 1: s_setprio 1 over the VN phase (0 over the CN phase), early stop and fixed count: config [3] 66.9 -> 67.5 M
 // cw/s (A/B profiles/r04/ab/ab_prio.txt); 2: the reverse (-1.3 %)
@@ -214,8 +219,14 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
             int t = z + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const int64_t o = (int64_t)j * Z + t;
+#if QC_PK_DIAG == 2  // DIAGNOSTIC BUILD ONLY (wrong results): no LLR loads, to price them
+            const float x0 = v0 ? (float)((z * 7 + j) % 9) - 4.0f : 0.0f;
+            const float x1 = v1 ? (float)((z * 5 + j) % 9) - 4.0f : 0.0f;
+            (void)o;
+#else
             const float x0 = v0 ? llr[cw0 * N + o] : 0.0f;
             const float x1 = v1 ? llr[(cw0 + 1) * N + o] : 0.0f;
+#endif
             const float q0 = fminf(fmaxf(rintf(x0 * qinv), -qmax), qmax);
             const float q1 = fminf(fmaxf(rintf(x1 * qinv), -qmax), qmax);
             L[j] = pk2(-q0, -q1);
@@ -406,7 +417,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
             if (k == 0 ? ok0 : ok1) {
                 const int64_t oo = (c0 + k) * N + o;
                 const float zz = 0.5f * (float)hv[k];
-                if (bits) bits[oo] = (uint8_t)(zz <= kZthrF32);
+                if (bits && QC_PK_DIAG != 1) bits[oo] = (uint8_t)(zz <= kZthrF32);  // DIAG 1: no output, to price it
                 if (soft) soft[oo] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + expf(-zz));
             }
         }

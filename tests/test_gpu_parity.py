@@ -534,6 +534,38 @@ def test_packed_quantized_ragged_batches(code, B, early):
     assert np.array_equal(bits[:B].cpu().numpy(), ref["bits"])
 
 
+@pytest.mark.parametrize("code", ["wifi648_12", "wifi1296_23"])
+def test_packed_quantized_io_alignment(code):
+    """LLR and bit buffers at any alignment (the ABI takes plain pointers: views into larger buffers), a ragged
+    B, bits only and with soft output: bit-identical to the oracle, and nothing outside [bits, bits + B * n)
+    is written.  (16-byte vector loads / stores staged through LDS were measured 1-2 % slower for this kernel,
+    DESIGN.md §3.3, so there is one per-element path.)"""
+    H, _ = get_code(code)
+    n = H.shape[1]
+    B = 37
+    cw, llr = _llr(H, B, 3.0, seed=77, rate=1 - H.shape[0] / n)
+    q = np.clip(np.rint(llr), -15, 15).astype(np.int8)
+    dec = ldpc_amd.get_decoder(H)
+    for early in (False, True):
+        ref = oracle.qms(H, q, 20, 15, 127, 0, early_stop=early)
+        for xoff, boff, soft in ((0, 0, "none"), (1, 0, "none"), (0, 3, "none"), (2, 9, "z"), (0, 0, "z")):
+            xs = torch.zeros(B * n + 8, dtype=torch.float32, device="cuda")
+            xs[xoff:xoff + B * n] = torch.from_numpy(llr.reshape(-1)).cuda()
+            bs = torch.full((B * n + 64,), 7, dtype=torch.uint8, device="cuda")
+            sf = torch.zeros((B, n), dtype=torch.float32, device="cuda")
+            p = dec.params(20, "qminsum", 15.0, 1.0, 0.0, early, "f32", soft, device_ptrs=True)
+            ws = torch.empty((max(dec.workspace_bytes(B, p), 1),), dtype=torch.uint8, device="cuda")
+            _abi.check(dec.lib.ldpc_decode_ex(dec._h, xs.data_ptr() + 4 * xoff, B, p, bs.data_ptr() + boff,
+                                              sf.data_ptr() if soft != "none" else 0, 0, ws.data_ptr(), ws.numel(),
+                                              torch.cuda.current_stream().cuda_stream))
+            torch.cuda.synchronize()
+            got = bs.cpu().numpy()
+            assert (got[:boff] == 7).all() and (got[boff + B * n:] == 7).all(), (xoff, boff, soft)
+            assert np.array_equal(got[boff:boff + B * n].reshape(B, n), ref["bits"]), (xoff, boff, soft, early)
+            if soft != "none":
+                assert np.array_equal(sf.cpu().numpy(), (0.5 * ref["app"]).astype(np.float32))
+
+
 def test_decode_llr_sign_convention():
     """decode(..., llr_sign="p0/p1") takes the communications convention (positive = bit 0): the same bits
     as the reference convention on the negated input."""

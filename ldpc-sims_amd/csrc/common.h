@@ -111,8 +111,9 @@ __device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
 // cancellation near |p| -> 1.  The VC side hands the check a signed a = copysign(exp(-|s|), s), s = L +
 // exclusive sum (twice the reference's tanh argument: |tanh(s/2)| = (1-a)/(1+a)).  A set of edges is a pair
 // (D, S) ~ (P+ - P-, P+ + P-) with P+- = prod(1 +- a); the identity is (0, 1), one edge adds D' = D + a*S,
-// S' = S + a*D (two fma), two sets join as D = Dp*Sq + Sp*Dq, S = Sp*Sq + Dp*Dq (products, then one add —
-// symmetric, so an edge with s = +-0, a = 1, keeps D == S exactly).  The check output of an edge is
+// S' = S + a*D (two fma), two sets join as D = Dp*Sq + Sp*Dq, S = Sp*Sq + Dp*Dq (one product and one fma
+// each, ds_join_out; an edge with s = +-0, a = 1, keeps D == S exactly through pushes and as a join's suffix,
+// to an ulp as its prefix).  The check output of an edge is
 // log(S/D) of the set of the others (= log((1+|p|)/(1-|p|))), at most log RMAX where RMAX =
 // (1+pmax)/(1-pmax) = 16777215 is the reference's fp32 p clamp (bp_cv.py:44-47) exactly, and at most the
 // caller's clamp (bp.py:47); its sign the xor of the others' signs.
@@ -204,10 +205,23 @@ __device__ __forceinline__ float ds_out(float D, float S, uint32_t sgn, float cm
     const float y = __builtin_amdgcn_fmed3f(__builtin_amdgcn_logf(r), 0.0f, cmax2);
     return u2f(f2u(y) | (sgn & 0x80000000u));
 }
-// the output of an edge from its prefix set p and suffix set q (the join, then ds_out)
+// the output of an edge from its prefix set p and suffix set q (the join, then ds_out).  DS_JOIN_FMA: each of
+// D and S is one product and one fma (D = fma(p.D, q.S, p.S * q.D), S = fma(p.D, q.D, p.S * q.S)), 4 VALU per
+// join instead of 6 (two products and an add each); both round at most twice, as before.  A symmetric suffix
+// (q.D == q.S: it holds an edge with a = 1, s = +-0) still gives D == S exactly — both are fma(p.D, x, p.S * x)
+// — so such an edge zeroes the others' outputs as the reference's p = 0; a symmetric prefix gives D, S within
+// an ulp (an output <= 2^-23 in log2 units instead of 0).  The oracle (ldpc_oracle.c cn_stable_f32) joins the same way.
+#ifndef DS_JOIN_FMA
+#define DS_JOIN_FMA 1
+#endif
 __device__ __forceinline__ float ds_join_out(DSet p, DSet q, uint32_t sgn, float cmax2) {
+#if DS_JOIN_FMA
+    const float D = __builtin_fmaf(p.D, q.S, p.S * q.D);
+    const float S = __builtin_fmaf(p.D, q.D, p.S * q.S);
+#else
     const float D = p.D * q.S + p.S * q.D;  // -ffp-contract=off: two products and one add each
     const float S = p.S * q.S + p.D * q.D;
+#endif
     return ds_out(D, S, sgn, cmax2);
 }
 

@@ -37,22 +37,23 @@ import numpy as np
 
 TOL = 1e-5
 # (kind, golden set, implementation) -> (entries where the reference's fp32 is within 1e-5 and ours is not, the
-# maximum error on decoding failures): measured (GPU: gpurun_out/r4a soft_parity.jsonl, round 4, every kernel
-# family; oracle: the CPU suite), the maxima rounded up in the third digit.  Unlisted sets: count 0.
+# maximum error on decoding failures): measured with the fma join (common.h DS_JOIN_FMA; GPU: the -m gpu suite
+# under LDPC_PARITY_MEASURE=1, every kernel family, profiles/r04/failure_bounds/; oracle: the CPU suite), collected
+# by scripts/failure_bounds.py, the maxima rounded up in the third digit.  Unlisted sets: count 0.
 FAILURE_BOUNDS = {
-    ("z", "wifi648_12_sp_it50 snr1", "gpu"): (430, 1.19e-4),
-    ("p1", "wifi648_12_sp_it50 snr1", "gpu"): (35, 2.89e-5),
-    ("z", "wifi648_12_sp_it50 snr2", "gpu"): (18, 1.18e-3),
-    ("p1", "wifi648_12_sp_it50 snr2", "gpu"): (22, 2.75e-4),
-    ("z", "wifi648_12_sp_it50_cl20 snr2", "gpu"): (15, 7.21e-4),
-    ("p1", "wifi648_12_sp_it50_cl20 snr2", "gpu"): (14, 1.70e-4),
-    ("z", "wifi1296_23_sp_it20 snr2", "gpu"): (1, 1.10e-5),
-    ("z", "wifi648_12_sp_it50 snr1", "oracle"): (64, 9.24e-5),
-    ("p1", "wifi648_12_sp_it50 snr1", "oracle"): (2, 2.12e-5),
-    ("z", "wifi648_12_sp_it50 snr2", "oracle"): (17, 5.22e-4),
-    ("p1", "wifi648_12_sp_it50 snr2", "oracle"): (10, 1.23e-4),
-    ("z", "wifi648_12_sp_it50_cl20 snr2", "oracle"): (14, 3.42e-4),
-    ("p1", "wifi648_12_sp_it50_cl20 snr2", "oracle"): (9, 8.02e-5),
+    ("z", "wifi648_12_sp_it50 snr1", "gpu"): (281, 1.94e-4),
+    ("p1", "wifi648_12_sp_it50 snr1", "gpu"): (24, 4.45e-5),
+    ("z", "wifi648_12_sp_it50 snr2", "gpu"): (19, 3.84e-4),
+    ("p1", "wifi648_12_sp_it50 snr2", "gpu"): (21, 8.02e-5),
+    ("z", "wifi648_12_sp_it50_cl20 snr2", "gpu"): (17, 3.63e-4),
+    ("p1", "wifi648_12_sp_it50_cl20 snr2", "gpu"): (16, 8.13e-5),
+    ("z", "wifi1296_23_sp_it20 snr2", "gpu"): (1, 1.12e-5),
+    ("z", "wifi648_12_sp_it50 snr1", "oracle"): (97, 6.67e-5),
+    ("p1", "wifi648_12_sp_it50 snr1", "oracle"): (2, 1.53e-5),
+    ("z", "wifi648_12_sp_it50 snr2", "oracle"): (22, 8.85e-4),
+    ("p1", "wifi648_12_sp_it50 snr2", "oracle"): (29, 2.21e-4),
+    ("z", "wifi648_12_sp_it50_cl20 snr2", "oracle"): (18, 6.87e-4),
+    ("p1", "wifi648_12_sp_it50_cl20 snr2", "oracle"): (27, 1.71e-4),
 }
 
 
@@ -145,6 +146,8 @@ def _check_failures(rec, kind, got_max, ref_env, count_key, tol):
     label = rec["label"]
     assert got_max <= max(tol, ref_env), f"{label}: {kind} on decoding failures outside max({tol}, the reference's " \
                                          f"own fp32 error there): {rec}"
+    if os.environ.get("LDPC_PARITY_MEASURE"):  # re-measuring FAILURE_BOUNDS (scripts/failure_bounds.py): (i) only
+        return
     count_m, max_m = _bounds(kind, label) or (0, max(tol, ref_env))
     assert rec[count_key] <= count_m, f"{label}: {rec[count_key]} {kind} entries where the reference's fp32 meets " \
                                       f"{tol} and ours does not (measured bound {count_m}): {rec}"

@@ -81,7 +81,9 @@ def main():
     # counters over gloo); the driver's multi-GPU runs use the defaults: one GPU per rank, RCCL.
     local = local % max(1, torch.cuda.device_count()) if os.environ.get("LDPC_BENCH_SHARE_GPU") else local
     torch.cuda.set_device(local)
-    if world > 1:
+    # LDPC_BENCH_PG=1: a process group even at world size 1 — the RCCL path (init, barriers, the rank gather)
+    # on a 1-GPU box, where RCCL refuses two ranks on one device (tests/test_gpu_multirank.py)
+    if world > 1 or os.environ.get("LDPC_BENCH_PG") == "1":
         backend = os.environ.get("LDPC_BENCH_BACKEND", "nccl")  # nccl == RCCL over xGMI
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -144,7 +146,7 @@ def main():
             "ber": ber,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -282,7 +284,7 @@ class Workload:
         torch.cuda.synchronize()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -291,7 +293,7 @@ class Workload:
             self.step(self.llrs[s % P])
         ev1.record(self.stream)
         torch.cuda.synchronize()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         mine = time.perf_counter() - t0
         gpu_ms = ev0.elapsed_time(ev1) / max(steps, 1)
@@ -323,7 +325,7 @@ def rank_evidence(world, rank, local, elapsed):
     me = {"rank": rank, "local_rank": local, "device": local, "name": props.name,
           "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")),
           "timed_s": elapsed}
-    if world > 1 and dist.is_initialized():
+    if dist.is_initialized():
         allr = [None] * dist.get_world_size()
         dist.all_gather_object(allr, me)
         return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()), "per_rank": allr}

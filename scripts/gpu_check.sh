@@ -11,6 +11,5 @@ timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail 
 python -c "
 import json; d=json.load(open('$OUT/bench.json'))
 print('headline', round(d['value']/1e6,2), 'M', d['ms_per_step'], 'ms', 'roofline', d['roofline']['bound'], round(d['roofline']['frac'],3))
-s=d['side']; print('tanh', round(s['gpu_tanh_sp']['value']/1e6,2) if isinstance(s.get('gpu_tanh_sp'),dict) else s.get('gpu_tanh_sp'))
-for k,v in s.get('configs',{}).items(): print(k, v.get('value'), v.get('unit'), v.get('ms_per_launch'), v.get('roofline',{}).get('bound'), v.get('roofline',{}).get('frac'))
-"
+s=d['side']; print('tanh', round(s['gpu_tanh_sp']['cw_per_s']/1e6,2), 'M')
+for k,v in s.get('configs',{}).items(): print(k, round(v['value']/1e6,3), 'M', round(v['ms_per_step'],3), 'ms', v['roofline']['bound'], round(v['roofline']['frac'],3))"

@@ -123,3 +123,26 @@ def test_bench_multigpu_runs_the_config4_leg():
     assert l2["ber"]["coded_ber_info"] == l1["ber"]["coded_ber_info"]
     assert l2["ber"]["coded_bler"] == l1["ber"]["coded_bler"]
     assert l2["roofline"]["bound"] == "hbm" and l2["roofline"]["frac"] > 0
+
+
+def test_bench_rccl_process_group_on_one_gpu():
+    """The RCCL path itself on the real device: bench.py under a process group with the default backend
+    ("nccl" = RCCL) at world size 1 (LDPC_BENCH_PG=1; RCCL refuses two ranks on one GPU — "Duplicate GPU
+    detected", scripts/rccl_probe.py — so the 2-rank tests above reduce over gloo).  The group initialises
+    with the decode device, the timed region's barriers and the rank gather run over RCCL, and the record
+    reports backend nccl with this GPU; the counts equal a run without a process group."""
+    common = ["bench.py", "--steps", "2", "--warmup", "1", "--iters", "10", "--ebn0", "1:1:3", "--batch", "4096",
+              "--no-cpu-baseline", "--no-legs", "--no-dropin"]
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", LOCAL_WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), LDPC_BENCH_PG="1", PYTHONPATH=os.path.join(ROOT, "ldpc-sims_amd"))
+    for k in ("LDPC_BENCH_BACKEND", "LDPC_BENCH_SHARE_GPU"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, *common], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    pg = _bench_line(p.stdout)
+    plain = _bench_line(_launch(common, 1))
+    rk = pg["ranks"]
+    assert rk["world_size"] == 1 and rk["backend"] == "nccl" and rk["per_rank"][0]["rank"] == 0
+    assert rk["per_rank"][0]["name"] == plain["ranks"]["per_rank"][0]["name"]
+    assert plain["ranks"]["backend"] is None
+    assert pg["ber"] == plain["ber"] and pg["value"] > 0

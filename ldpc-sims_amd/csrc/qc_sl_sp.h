@@ -333,7 +333,12 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
 #define QC_RS_ADDR_OPAQUE 0  // 1: address VGPRs through an empty asm at each use (a v_mov each: 4.09 vs 4.28 M cw/s)
 #endif
 #ifndef QC_RS_DS_BLOCK
-#define QC_RS_DS_BLOCK 10  // check rows of d = 20 in two blocks (common.h cn_ds_row): 4.27 -> 4.33 M cw/s (7: 3 blocks)
+// check rows (d = 20) in blocks of this many edges (common.h cn_ds_row; bitwise the same outputs).  20: one block,
+// no shared suffix pass — with the fma join 4.96 -> 5.30 M cw/s (1,279 -> 1,182 VALU per wave-iteration); 16: 5.18,
+// 14: 5.13 (no spill); 7: 4.86 (profiles/r04/ab/ab_rs2.txt).  At 20, five VGPRs (values set before the iteration
+// loop and read after it) go to scratch around the loop — no scratch access inside it (tests/test_kernel_resources.py);
+// recomputing the output indices after the loop moved a spill INTO the loop instead.
+#define QC_RS_DS_BLOCK 20
 #endif
 #ifndef QC_RS_PRIO
 // 1: s_setprio 1 over the latency-bound VN phase (short chains between LDS loads), 0 over the issue-bound CN phase,

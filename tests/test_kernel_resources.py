@@ -1,9 +1,13 @@
 """Every kernel a BASELINE.json configuration dispatches is spill-free: no VGPR spills and no scratch, read
 from the gfx950 code objects' AMDGPU metadata notes of the built libldpc_hip.so (no GPU needed;
 scripts/kernel_resources.py).  SGPR spills go to VGPR lanes (v_writelane), not to memory, and are allowed.
+One exception, checked on the disassembly instead: config [2]'s resident kernel keeps a few values set before
+its iteration loop and read after it in scratch (one-block check rows, qc_sl_sp.h QC_RS_DS_BLOCK) — no scratch
+access inside the loop.
 
     [1] (648,1/2) min-sum 50 it          k_qc_ms_ph<Wifi648_12, false, false, 0>
-    [2] (1944,5/6) tanh-SP, 16-QAM OFDM   k_qc_sp_sl<Wifi1944_56, *> (fixed; early stop too)
+    [2] (1944,5/6) tanh-SP, 16-QAM OFDM   k_qc_sp_rs<Wifi1944_56> (fixed count), k_qc_sp_sl<Wifi1944_56, *>
+                                          (early stop; the fixed-count sliced kernel remains for QC_SL_SP_RS=0)
     [3] (1296,2/3) 5-bit min-sum 20 it ES k_qc_qms_pk<Wifi1296_23, *, *>  (packed fp16, two codewords per lane)
     [4] DVB-S2 64800 rate 1/2, 50 it      generic CSR kernels at degree bound 8 (k_vn_ms/k_cn_ms, k_vn_sp/k_cn_sp),
                                           k_load_llr, k_final
@@ -31,6 +35,7 @@ BASELINE_KERNELS = [
     r"k_final<float, 32, (true|false)>",
     r"k_qc_sp_st<ldpc::Wifi648_12, false>",
 ]
+MAX_SPILL_OUTSIDE_LOOP = {r"k_qc_sp_rs<ldpc::Wifi1944_56>": 8}
 
 
 @pytest.fixture(scope="module")
@@ -52,6 +57,22 @@ def test_baseline_config_kernels_do_not_spill(resources, pattern):
     for d, r in hits.items():
         assert r.get("vgpr_spill_count", 0) == 0, (d, r)
         assert r.get("private_segment_fixed_size", 0) == 0, (d, r)
+
+
+@pytest.mark.parametrize("pattern", sorted(MAX_SPILL_OUTSIDE_LOOP))
+def test_resident_kernel_spills_only_outside_the_iteration_loop(resources, pattern):
+    """At most the listed number of spilled VGPRs, and no scratch instruction inside the kernel's iteration
+    loop (its longest backward branch, scripts/isa_mix.py), so the loop runs from registers and LDS only."""
+    import kernel_resources as kr
+    from isa_mix import kernel_lines, main_loop
+    hits = {d: r for d, r in resources.items() if re.search(r"ldpc::" + pattern, d)}
+    assert len(hits) == 1, hits
+    (d, r), = hits.items()
+    assert r.get("vgpr_spill_count", 0) <= MAX_SPILL_OUTSIDE_LOOP[pattern], (d, r)
+    _, lines = kernel_lines(kr.DEFAULT_LIB, "k_qc_sp_rs")
+    loop = main_loop(lines)
+    assert len(loop) > 1000, len(loop)
+    assert not [op for _, op, _, _ in loop if op.startswith("scratch_")], "scratch access inside the loop"
 
 
 GENERIC_KERNELS = r"ldpc::k_(vn_sp|vn_spw|cn_sp|vn_ms|cn_ms|final|load_llr)<"

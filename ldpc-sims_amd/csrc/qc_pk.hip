@@ -37,6 +37,19 @@ namespace ldpc {
 #ifndef QC_PK_LDSROT_EARLY
 #define QC_PK_LDSROT_EARLY 0
 #endif
+// QC_PK_DROT(_EARLY): lane rotations through a per-wave DOUBLED LDS row: every active lane stores its value at
+// slots z and z + Z of its lane group's row with one ds_write2_b32, and reads slot z + rho (< 2Z: no wrap, so no
+// per-rotation address select and no address registers — the offset is the ds immediate); idle lanes write and
+// read a private dummy stretch.  A wave's LDS operations run in order, so the row needs no barrier.  Bitwise the
+// same results (every packed / quantized parity test passes on it) with 84 fewer VALU per wave-iteration, but
+// slower: config [3] 67.3 -> 62.1 M cw/s, fixed count 53.5 -> 50.8, (648,1/2) early stop 114.7 -> 107.9 (A/B
+// profiles/r04/ab/ab_drot.txt) — a rotation's store-then-load round trip sits on the chain ds_bpermute shortens.
+#ifndef QC_PK_DROT
+#define QC_PK_DROT 0
+#endif
+#ifndef QC_PK_DROT_EARLY
+#define QC_PK_DROT_EARLY 0
+#endif
 #ifndef QC_PK_WAVES_PER_SIMD
 #define QC_PK_WAVES_PER_SIMD 4
 #endif
@@ -189,13 +202,23 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     int ra[Z];
     static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
         constexpr int rho = decltype(rr)::value;
-        if constexpr (rot_uses<C>(rho) >= MINU)
+        if constexpr (rot_uses<C>(rho) >= MINU && !(EARLY ? QC_PK_DROT_EARLY : QC_PK_DROT))
             ra[rho] = sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho;
     });
+    constexpr bool DROT = EARLY ? QC_PK_DROT_EARLY : QC_PK_DROT;
+    constexpr int DW = CPW * 2 * Z + 64 + 2 * Z;  // words per wave: doubled rows, then the idle lanes' stretch
+    __shared__ uint32_t Rd[DROT ? (pk_tpb<EARLY>() / 64) * DW : 1];
+    const int da = DROT ? 4 * ((int)(threadIdx.x >> 6) * DW + ((z < Z) ? half * 2 * Z + z : CPW * 2 * Z + lane)) : 0;
     auto rot = [&](auto rr, uint32_t x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
         constexpr int rho = decltype(rr)::value;
         if constexpr (rho == 0) {
             return x;
+        } else if constexpr (DROT) {
+            static_assert(4 * Z <= 255 * 4, "ds_write2 offset1 is 8 bits (in dwords)");
+            asm volatile("ds_write2_b32 %0, %1, %1 offset1:%2" ::"v"((unsigned)(uintptr_t)&Rd[0] + (unsigned)da), "v"(x),
+                         "i"(Z)
+                         : "memory");
+            return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(Rd) + da + 4 * rho);
         } else if constexpr (rot_uses<C>(rho) >= MINU) {
             return xfer(ra[rho], x);
         } else {

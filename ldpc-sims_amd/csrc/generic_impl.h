@@ -80,6 +80,12 @@ __device__ __forceinline__ bool tile_slot(int nodes, int tpl2, int64_t B, int& n
 // GEN_SKIP_DUP: the min-sum kernels load only the d < MAXD edges a node has (d is wave-uniform: a scalar
 // branch per slot) instead of re-loading the last edge into the unused slots (cache hits, but TA / L2 requests:
 // DVB-S2's variables have degree 8, 3 or 2 under MAXD = 8)
+#ifndef GEN_VW_CAP
+#define GEN_VW_CAP 16  // A/B knob: at most this many codewords per thread in the streaming kernels' wide tiles
+#endif
+#ifndef GEN_TPL2_MAX
+#define GEN_TPL2_MAX 8  // A/B knob: at most 2^GEN_TPL2_MAX threads per node (the rest of the 256 take other nodes)
+#endif
 #ifndef GEN_SKIP_DUP
 #define GEN_SKIP_DUP 0
 #endif
@@ -672,9 +678,11 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     // tiles: wide (V = VW codewords per thread) when a wave's 64 lanes have >= 64*VW codewords to cover,
     // else narrow (V = 1); 2^tpl2 threads per node
     auto tile = [B](int vw, int& V, int& tpl2) {
+        vw = vw < GEN_VW_CAP ? vw : GEN_VW_CAP;
         V = (B >= 64 * vw) ? vw : 1;
         const int64_t lanes = (B + V - 1) / V;
         tpl2 = lanes > 128 ? 8 : lanes > 64 ? 7 : 6;
+        tpl2 = tpl2 < GEN_TPL2_MAX ? tpl2 : GEN_TPL2_MAX;
     };
     auto grid = [B](int V, int tpl2, int nodes) {
         return dim3((unsigned)((B + ((int64_t)V << tpl2) - 1) / ((int64_t)V << tpl2)),

@@ -94,3 +94,28 @@ def test_config2_kernels_agree_at_50_iterations():
         b = dec.decode(x, 50, algo="tanh", clamp=20.0, soft="z", force_generic=True)
         assert torch.equal(a["bits"], b["bits"])
         assert torch.equal(a["soft"].view(torch.int32), b["soft"].view(torch.int32))
+
+
+@pytest.mark.parametrize("B", [1, 2, 3])
+def test_config2_resident_kernel_tiny_batches_write_nothing_past_B(B):
+    """The resident kernel decodes codeword pairs (one unit = two codewords in the lane halves): B = 1 and 3
+    leave the last unit's second codeword absent.  Bits and z bitwise equal to the generic CSR path, and the
+    rows after B of larger output buffers stay untouched."""
+    from ldpc_amd import _abi
+    H, _ = get_code("wifi1944_56")
+    n = H.shape[1]
+    dec = ldpc_amd.get_decoder(H)
+    _, x = _qam16_llrs(H, B, 6.0, seed=90 + B)
+    a = dec.decode(x, 50, algo="tanh", clamp=20.0, soft="z")
+    g = dec.decode(x, 50, algo="tanh", clamp=20.0, soft="z", force_generic=True)
+    assert torch.equal(a["bits"], g["bits"]) and torch.equal(a["soft"].view(torch.int32), g["soft"].view(torch.int32))
+    p = dec.params(50, "tanh", 20.0, 1.0, 0.0, False, "f32", "z", device_ptrs=True)
+    bits = torch.full((B + 2, n), 7, dtype=torch.uint8, device="cuda")
+    soft = torch.full((B + 2, n), 7.0, dtype=torch.float32, device="cuda")
+    used = torch.full((B + 2,), 77, dtype=torch.int32, device="cuda")
+    ws = torch.empty((max(dec.workspace_bytes(B, p), 1),), dtype=torch.uint8, device="cuda")
+    _abi.check(dec.lib.ldpc_decode_ex(dec._h, x.data_ptr(), B, p, bits.data_ptr(), soft.data_ptr(), used.data_ptr(),
+                                      ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    assert (bits[B:] == 7).all() and (soft[B:] == 7.0).all() and (used[B:] == 77).all()
+    assert torch.equal(bits[:B], a["bits"]) and (used[:B] == 50).all()

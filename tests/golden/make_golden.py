@@ -27,11 +27,14 @@ What it records (all .npz, numeric arrays only — loadable with allow_pickle=Fa
   * bp_<code>_sp.npz       802.11n (648,1/2), (1296,2/3), (1944,5/6): p1 and z, 5 iterations, clamp 10.
   * bp_<code>_sp_it<k>.npz the same at 50 / 20 / 10 iterations (one reference layer looped, checked bitwise
                            against BeliefPropagation(H, 5) first).
+  * bp_wifi1944_56_sp_it50_cl20.npz  BASELINE config [2]: (1944,5/6) 50 iterations, clamp 20, 16-QAM OFDM LLRs
+                           from the on-device front end (c2_16qam_llrs.npz, scripts/gen_c2_llrs_gpu.py): fp32,
+                           .double() and the f32-bound .double() (wifi1944c2).
   * bp_wifi648_12_sp_it50_cl20.npz  (648,1/2) 50 iterations at clamp 20, above the p-clamp ceiling; plus
                            (wificlampb32) the reference's .double() module with the fp32 module's p-clamp bound
                            swapped in at run time (f32_pclamp): p1_f64b32_* / z_f64b32_*.
 
-    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32]
+    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32] [wifi1944c2]
 """
 import contextlib
 import os
@@ -404,6 +407,50 @@ def gen_wifi_clamp_f32bound():
     np.savez_compressed(path, **d)
 
 
+def gen_wifi1944_c2(llr_path=os.path.join(HERE, "c2_16qam_llrs.npz")):
+    """bp_wifi1944_56_sp_it50_cl20.npz: BASELINE config [2] at its own settings through the reference itself —
+    (1944,5/6), tanh-SP 50 iterations, clamp 20 (the config [2] leg's), on 16-QAM OFDM LLRs from the on-device
+    front end (scripts/gen_c2_llrs_gpu.py -> c2_16qam_llrs.npz: 16 codewords at 6.0 / 6.5 dB, the waterfall):
+    the fp32 module, .double(), and .double() with the fp32 module's p-clamp bound (f32_pclamp, the fp64 target
+    above the ceiling), one reference layer looped (run_ref_looped; checked against BeliefPropagation(H, 5) in
+    gen_wifi_sp_long)."""
+    from ldpc_amd.codes import get_code
+    src = np.load(llr_path)
+    H, qc = get_code("wifi1944_56")
+    H = np.asarray(H, dtype=np.int64)
+    iters, clamp, chunk = 50, 20.0, 8
+    model = BeliefPropagation(H, 1)
+    model.eval()
+    rec = {}
+    for snr in src["snrs"]:
+        tag = f"snr{snr:g}".replace(".", "p")
+        llr = src[f"llr_{tag}"].astype(np.float32)
+        cw = src[f"codeword_{tag}"]
+        outs = {k: [] for k in ("p32", "z32", "p64", "z64", "pb", "zb")}
+        for s in range(0, llr.shape[0], chunk):
+            p32, z32 = run_ref_looped(model.float(), iters, clamp, llr[s:s + chunk])
+            p64, z64 = run_ref_looped(model.double(), iters, clamp, llr[s:s + chunk], double=True)
+            with f32_pclamp() as hits:
+                pb, zb = run_ref_looped(model.double(), iters, clamp, llr[s:s + chunk], double=True)
+            assert hits[0] == iters, hits
+            for k, v in zip(("p32", "z32", "p64", "z64", "pb", "zb"), (p32, z32, p64, z64, pb, zb)):
+                outs[k].append(v)
+        p32, z32, p64, z64, pb, zb = (np.concatenate(outs[k]) for k in ("p32", "z32", "p64", "z64", "pb", "zb"))
+        rec[f"llr_{tag}"] = llr
+        rec[f"codeword_{tag}"] = cw.astype(np.uint8)
+        rec[f"p1_f32_{tag}"] = p32.astype(np.float32)
+        rec[f"z_f32_{tag}"] = z32.astype(np.float32)
+        rec[f"p1_f64_{tag}"] = p64
+        rec[f"z_f64_{tag}"] = z64
+        rec[f"p1_f64b32_{tag}"] = pb
+        rec[f"z_f64b32_{tag}"] = zb
+        print("wifi1944_56 50 it clamp 20 16-QAM", tag, "bit errors:", int((np.round(p32) != cw).sum()),
+              "codeword errors:", int((np.round(p32) != cw).any(1).sum()), "of", cw.shape[0],
+              "|dz| f32 vs f32-bound f64", float(np.abs(z32 - zb).max()), flush=True)
+    np.savez_compressed(os.path.join(HERE, "bp_wifi1944_56_sp_it50_cl20.npz"), base=qc.base, Z=qc.Z, iters=iters,
+                        clamp=clamp, snrs=np.array(src["snrs"]), chunk=chunk, **rec)
+
+
 def gen_x0():
     """bp_x0.npz: the reference forward with NON-ZERO initial messages x (bp/bp.py:43-47), which the first
     layer consumes like any later one: (64,32) at iterations 0 / 1 / 5 and (648,1/2) at 3, clamp 10, x drawn
@@ -434,10 +481,11 @@ def gen_x0():
 
 
 if __name__ == "__main__":
-    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong", "wificlamp", "wificlampb32"]
+    parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong", "wificlamp", "wificlampb32",
+                             "wifi1944c2"]
     for part in parts:
         {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp, "x0": gen_x0,
          "wifilong": gen_wifi_sp_long,
          "wificlamp": lambda: gen_wifi_sp_long(WIFI_SP_CLAMPS, clamp_tag=True),
-         "wificlampb32": gen_wifi_clamp_f32bound}[part]()
+         "wificlampb32": gen_wifi_clamp_f32bound, "wifi1944c2": gen_wifi1944_c2}[part]()
     print("done")

@@ -1,9 +1,10 @@
 """BASELINE config [2] at its own iteration count: 802.11n (1944,5/6) tanh sum-product, 50 iterations, on 16-QAM
 OFDM LLRs from the on-device front end — exactly the leg bench.py times (side.configs.config2) — against the C
 oracle's (D, S)-form fp32 restatement (oracle.sp_f32(stable=True), the kernels' specification; restating
-bp_vc.py:16-27 / bp_cv.py:22-50).  The reference's own goldens for this code stop at 10 iterations
-(tests/golden/bp_wifi1944_56_sp_it10.npz, test_gpu_parity.py); its dense E x E masks make 50 iterations of the
-(1944,5/6) module a 3-4 GB-per-layer forward, so the 50-iteration soft targets are the oracle's.
+bp_vc.py:16-27 / bp_cv.py:22-50), on 256 codewords per point.  The REFERENCE's own run of this configuration (32
+codewords of the same front end, one reference layer looped: tests/golden/bp_wifi1944_56_sp_it50_cl20.npz — bits,
+p1 and z against its fp32 module and the f32-bound .double()) is checked by tests/test_gpu_soft_parity.py with
+every other golden.
 
 Tolerances (the soft target is the fp64 evaluation of the same function, oracle.sp_f64 with the fp32 module's
 p-clamp bound since clamp 20 is above the ceiling — pinned to the reference's own fp64 module in

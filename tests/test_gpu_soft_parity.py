@@ -8,7 +8,9 @@ Goldens were produced by the reference itself (tests/golden/make_golden.py):
 * bp_<802.11n code>_sp_it<k>.npz: the same at the iteration counts the drop-in and the BASELINE configs run —
   (648,1/2) 50 iterations x 192 codewords, (1296,2/3) 20 x 96, (1944,5/6) 10 x 48, clamp 10;
 * bp_wifi648_12_sp_it50_cl20.npz: (648,1/2) 50 iterations, clamp 20 — above the p-clamp ceiling, where the z target
-  is the fp32 module's function in fp64 (softparity.f64_target).
+  is the fp32 module's function in fp64 (softparity.f64_target);
+* bp_wifi1944_56_sp_it50_cl20.npz: BASELINE config [2] at its own settings — (1944,5/6), 50 iterations, clamp 20,
+  16-QAM OFDM LLRs from the on-device front end, 16 codewords at 6.0 and 6.5 dB.
 Both kernel families run every file: the register/sliced QC kernels ("auto") and the generic CSR kernels.
 Hard decisions must equal the reference's fp32 hard decisions exactly.
 """

@@ -137,7 +137,7 @@ def test_oracle_wifi_codes_match_reference(path):
     d = np.load(path)
     H = qc_expand(d["base"], int(d["Z"]))
     iters, clamp = int(d["iters"]), float(d["clamp"])
-    assert len(WIFI_SP_FILES) == 7
+    assert len(WIFI_SP_FILES) == 8
     for snr in d["snrs"]:
         tag = f"snr{snr:g}".replace(".", "p")
         llr = d[f"llr_{tag}"]
@@ -179,14 +179,16 @@ def test_ceiling_golden_separates_f32_and_f64_modules():
     assert (np.abs(d["z_f32_snr3"] - t32) / np.maximum(1.0, np.abs(t32))).max() > 1e-3  # the fp32 module's own
 
 
-def test_oracle_f32_bound_f64_pinned_to_reference():
+@pytest.mark.parametrize("name", ["bp_wifi648_12_sp_it50_cl20.npz", "bp_wifi1944_56_sp_it50_cl20.npz"])
+def test_oracle_f32_bound_f64_pinned_to_reference(name):
     """Above the ceiling the soft target is the REFERENCE's own .double() module with the fp32 module's p-clamp
     bound swapped in at run time (make_golden.py f32_pclamp -> p1_f64b32_* / z_f64b32_*): the oracle's
     sp_f64(ceiling="f32") restates exactly that function — within fp64 rounding of the reference (<= 1e-9 in z over
     50 iterations, decoding failures included); and that target differs from the plain .double() module by the
-    ceiling alone (> 0.1 on ceiling-bound entries)."""
+    ceiling alone (> 0.1 on ceiling-bound entries).  Both clamp-20 files: (648,1/2) BPSK and BASELINE config [2]
+    ((1944,5/6), 16-QAM OFDM LLRs)."""
     from ldpc_amd.codes import qc_expand
-    d = np.load(os.path.join(GOLDEN, "bp_wifi648_12_sp_it50_cl20.npz"))
+    d = np.load(os.path.join(GOLDEN, name))
     H = qc_expand(d["base"], int(d["Z"]))
     for snr in d["snrs"]:
         tag = f"snr{snr:g}".replace(".", "p")
@@ -205,6 +207,11 @@ def test_looped_reference_golden_settings():
         d = np.load(os.path.join(GOLDEN, f"bp_{name}_sp_it{iters}.npz"))
         assert int(d["iters"]) == iters and float(d["clamp"]) == 10.0
         assert sum(d[f"llr_snr{s:g}".replace(".", "p")].shape[0] for s in d["snrs"]) == cws
+    # BASELINE config [2] at its own settings: (1944,5/6) tanh-SP 50 iterations, the leg's clamp 20, 16-QAM OFDM
+    # LLRs from the on-device front end, in the waterfall (6.0 / 6.5 dB: decoded and failing codewords both)
+    d = np.load(os.path.join(GOLDEN, "bp_wifi1944_56_sp_it50_cl20.npz"))
+    assert int(d["iters"]) == 50 and float(d["clamp"]) == 20.0 and int(d["Z"]) == 81
+    assert list(d["snrs"]) == [6.0, 6.5]
 
 
 def test_ds_form_identities():

@@ -624,6 +624,12 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
 #ifndef QC_PH_LDSROT
 #define QC_PH_LDSROT 1
 #endif
+#ifndef QC_SP_MASK_IDLE
+#define QC_SP_MASK_IDLE 0  // A/B neutral (+0.2 %, profiles/r04/ab/ab_mask.txt)
+#endif
+#ifndef QC_PH_MASK_IDLE
+#define QC_PH_MASK_IDLE 1  // A/B profiles/r04/ab/ab_mask.txt: +0.9 % (42.02 -> 42.39 M cw/s, three interleaved pairs), parity green
+#endif
 #ifndef QC_PH_XSEL
 #define QC_PH_XSEL 0  // compare-free check output in the lookahead loop (plain min-sum): A/B with LDS-row
                       // rotations 43.05 vs 43.13 M cw/s (removes the 60 hazard s_nops, same VALU count) — off
@@ -927,6 +933,10 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 #endif
 
     int it = 0;
+    // QC_PH_MASK_IDLE (fixed count): the idle lanes (z >= Z: 10 of 64 at Z = 27) sit the iteration loop out,
+    // EXEC-masked — no active lane ever reads them (rotation sources are active slots) — so they stop drawing power
+    const bool loop_lane = !(QC_PH_MASK_IDLE && !EARLY) || z < Z;
+    if (loop_lane) {
     for (; it + 1 < iters; ++it) {
 #if QC_PH_LA && QC_PH_APPB
         if constexpr (APPB) {
@@ -1040,6 +1050,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
             });
         }
     }
+    }  // loop_lane
     // last iteration (or early exit): outputs straight from the VN phase, column by column
     const bool early_exit = EARLY && done_groups == (G0 | G1);
     if (!early_exit && iters > 0) {
@@ -1204,6 +1215,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     uint64_t done_groups = 0;  // lane masks of converged codewords (CPW == 2)
     int used_lo = iters, used_hi = iters;
 
+    // QC_SP_MASK_IDLE (fixed count): idle lanes (z >= Z) sit the iteration loop out, EXEC-masked (as QC_PH_MASK_IDLE)
+    const bool loop_lane = !(QC_SP_MASK_IDLE && !EARLY) || z < Z;
+    if (loop_lane)
     for (int it = 0; it < iters; ++it) {
         if constexpr (EARLY) {
             if (it > 0) {

@@ -65,6 +65,9 @@ namespace ldpc {
 #ifndef QC_PK_ES_ROWS
 #define QC_PK_ES_ROWS 1  // early-stop syndrome row by row with an early exit (one codeword pair per wave, Z = 54)
 #endif
+#ifndef QC_PK_MASK_IDLE
+#define QC_PK_MASK_IDLE 0  // A/B -2 % on config [3] (profiles/r04/ab/ab_mask.txt)
+#endif
 #ifndef QC_PK_DIAG
 // DIAGNOSTIC BUILDS ONLY (wrong results; DESIGN.md §3.3, scripts/pk_floor_diag.sh): 1 = no bit stores, 2 = no
 // LLR loads — prices the per-launch data movement
@@ -324,6 +327,10 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     _Float16* Lh = reinterpret_cast<_Float16*>(Ls);
 
     int it = 0;
+    // QC_PK_MASK_IDLE: idle lanes (z >= Z) sit the iteration loop out, EXEC-masked (as qc.hip QC_PH_MASK_IDLE); the
+    // early-stop decisions come from ballots restricted to the active lanes, so they are unchanged
+    const bool loop_lane = !QC_PK_MASK_IDLE || z < Z;
+    if (loop_lane)
     for (; it + 1 < iters; ++it) {
         if constexpr (QC_PK_PRIO == 1) __builtin_amdgcn_s_setprio(0);
         if constexpr (QC_PK_PRIO == 2) __builtin_amdgcn_s_setprio(1);

@@ -346,6 +346,9 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
 // cw/s (A/B profiles/r04/ab/ab_rs.txt); 2: the reverse, 4.25; 3: as 1, and the CN phase's row gathers at 1 too
 #define QC_RS_PRIO 1
 #endif
+#ifndef QC_RS_MASK_IDLE
+#define QC_RS_MASK_IDLE 0  // A/B -1.5 % (profiles/r04/ab/ab_mask.txt)
+#endif
 #ifndef QC_RS_IDLE_DUP
 #define QC_RS_IDLE_DUP 0  // 1: idle lanes l >= 27 shadow lane l - 27 (same loads, same values) and store too: no exec branches
 #endif
@@ -504,6 +507,10 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
         return sp_z(Lr_at(j), Ssum);
     };
 
+    // QC_RS_MASK_IDLE: idle lanes (l >= ZL) sit the iteration loop out, EXEC-masked (they never store; every wave
+    // keeps live lanes, so each still meets both barriers of every iteration)
+    const bool loop_lane = !QC_RS_MASK_IDLE || live;
+    if (loop_lane)
     for (int it = 0; it < iters; ++it) {
         // VN phase (variable frame): every column's c2v -> v2c as signed a, written back in place
         if constexpr (QC_RS_PRIO == 1 || QC_RS_PRIO == 3) __builtin_amdgcn_s_setprio(1);

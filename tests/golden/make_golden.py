@@ -30,11 +30,14 @@ What it records (all .npz, numeric arrays only — loadable with allow_pickle=Fa
   * bp_wifi1944_56_sp_it50_cl20.npz  BASELINE config [2]: (1944,5/6) 50 iterations, clamp 20, 16-QAM OFDM LLRs
                            from the on-device front end (c2_16qam_llrs.npz, scripts/gen_c2_llrs_gpu.py): fp32,
                            .double() and the f32-bound .double() (wifi1944c2).
+  * e2e_wifi648_qpsk_ofdm.npz  the reference's whole receiver chain (bits, encode_bits, modulate_bits, gen_data's
+                           32-point OFDM over AWGN, demodulate_signal) into decode_bits(llrs, H, 50, 40, 10) on
+                           the (648,1/2) code, 96 rows per Es/N0 point (rows 80..95 stay 0) (e2e648).
   * bp_wifi648_12_sp_it50_cl20.npz  (648,1/2) 50 iterations at clamp 20, above the p-clamp ceiling; plus
                            (wificlampb32) the reference's .double() module with the fp32 module's p-clamp bound
                            swapped in at run time (f32_pclamp): p1_f64b32_* / z_f64b32_*.
 
-    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32] [wifi1944c2]
+    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32] [wifi1944c2] [e2e648]
 """
 import contextlib
 import os
@@ -451,6 +454,40 @@ def gen_wifi1944_c2(llr_path=os.path.join(HERE, "c2_16qam_llrs.npz")):
                         clamp=clamp, snrs=np.array(src["snrs"]), chunk=chunk, **rec)
 
 
+def gen_e2e648():
+    """e2e_wifi648_qpsk_ofdm.npz: the reference's whole receiver chain as its evaluate scripts run it
+    (evaluate_snr.py:43,89,122): np.random bits, encode_bits with a generator of the (648,1/2) code,
+    modulate_bits (QPSK), gen_data (32-point OFDM over AWGN, ofdm_functions.py:109-116) -> demodulate_signal LLRs,
+    then decode_bits(llrs, H, 50, 40, 10) — 96 codewords per Es/N0 point, so rows 80..95 (N % batch_size) stay 0.
+    Inputs are the reference's own float64 LLRs; outputs its float64 bits."""
+    from ldpc_amd.codes import get_code
+    H, qc = get_code("wifi648_12")
+    H = np.asarray(H, dtype=np.int64)
+    enc = Encoder(H)
+    G = enc.encode(np.eye(enc.k, dtype=np.int64)).T.astype(np.int64)        # (n, k): cw = G @ bits mod 2
+    assert not ((H @ G) % 2).any()
+    B, iters, bs, clamp, ofdm = 96, 50, 40, 10, 32
+    rec = {}
+    snrs = (1.0, 1.5)  # the waterfall: decoded and failing rows both
+    for snrdb in snrs:
+        np.random.seed(int(100 * snrdb) + 648)
+        bits = OF.create_bits(B * enc.k)
+        cbits = OF.encode_bits(bits, G)
+        tx = OF.modulate_bits(cbits)
+        _, _, rx_llrs, _ = OF.gen_data(tx, snrdb, ofdm)
+        llrs = rx_llrs.reshape((-1, H.shape[1]))
+        out = OF.decode_bits(llrs, H, iters, bs, clamp)
+        tag = f"snr{snrdb:g}".replace(".", "p")
+        rec[f"llrs_{tag}"] = llrs
+        rec[f"codeword_{tag}"] = cbits.reshape((-1, H.shape[1])).astype(np.uint8)
+        rec[f"out_{tag}"] = out
+        rows = (B // bs) * bs
+        print("e2e648", tag, "bit errors in decoded rows:", int((out[:rows] != rec[f"codeword_{tag}"][:rows]).sum()),
+              "tail zero:", not out[rows:].any(), flush=True)
+    np.savez_compressed(os.path.join(HERE, "e2e_wifi648_qpsk_ofdm.npz"), base=qc.base, Z=qc.Z, iters=iters,
+                        batch_size=bs, clamp=clamp, ofdm_size=ofdm, snrs=np.array(snrs), **rec)
+
+
 def gen_x0():
     """bp_x0.npz: the reference forward with NON-ZERO initial messages x (bp/bp.py:43-47), which the first
     layer consumes like any later one: (64,32) at iterations 0 / 1 / 5 and (648,1/2) at 3, clamp 10, x drawn
@@ -482,10 +519,10 @@ def gen_x0():
 
 if __name__ == "__main__":
     parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong", "wificlamp", "wificlampb32",
-                             "wifi1944c2"]
+                             "wifi1944c2", "e2e648"]
     for part in parts:
         {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp, "x0": gen_x0,
          "wifilong": gen_wifi_sp_long,
          "wificlamp": lambda: gen_wifi_sp_long(WIFI_SP_CLAMPS, clamp_tag=True),
-         "wificlampb32": gen_wifi_clamp_f32bound, "wifi1944c2": gen_wifi1944_c2}[part]()
+         "wificlampb32": gen_wifi_clamp_f32bound, "wifi1944c2": gen_wifi1944_c2, "e2e648": gen_e2e648}[part]()
     print("done")

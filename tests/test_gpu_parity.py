@@ -566,6 +566,21 @@ def test_packed_quantized_io_alignment(code):
                 assert np.array_equal(sf.cpu().numpy(), (0.5 * ref["app"]).astype(np.float32))
 
 
+def test_decode_bits_reference_receiver_chain_golden():
+    """The drop-in on the reference's own receiver chain (tests/golden/e2e_wifi648_qpsk_ofdm.npz: the reference's
+    bits -> encode_bits -> modulate_bits -> gen_data's 32-point OFDM over AWGN -> demodulate_signal LLRs ->
+    decode_bits(llrs, H, 50, 40, 10), evaluate_snr.py's pipeline) on (648,1/2) in the waterfall: the float64 output
+    equals the reference's exactly — decoded and failing rows, and the zero tail rows 80..95."""
+    from ldpc_amd.codes import qc_expand
+    d = np.load(os.path.join(GOLDEN, "e2e_wifi648_qpsk_ofdm.npz"))
+    H = qc_expand(d["base"], int(d["Z"]))
+    for snr in d["snrs"]:
+        tag = f"snr{snr:g}".replace(".", "p")
+        out = ldpc_amd.decode_bits(d[f"llrs_{tag}"], H, int(d["iters"]), int(d["batch_size"]), int(d["clamp"]))
+        assert out.dtype == np.float64 and out.shape == d[f"out_{tag}"].shape
+        assert np.array_equal(out, d[f"out_{tag}"]), tag
+
+
 def test_decode_llr_sign_convention():
     """decode(..., llr_sign="p0/p1") takes the communications convention (positive = bit 0): the same bits
     as the reference convention on the negated input."""

@@ -200,6 +200,24 @@ def test_oracle_f32_bound_f64_pinned_to_reference(name):
         assert np.array_equal(r["bits"], np.round(d[f"p1_f64b32_{tag}"]).astype(np.uint8))
 
 
+def test_oracle_reference_receiver_chain_golden():
+    """e2e_wifi648_qpsk_ofdm.npz: the reference's own receiver chain (QPSK, 32-point OFDM, demodulate_signal)
+    into decode_bits(llrs, H, 50, 40, 10) — the oracle's restatement of the reference's fp32 operations decodes
+    the decoded rows' LLRs to the same bits (failures included); the tail rows are 0 in the reference's output."""
+    from ldpc_amd.codes import qc_expand
+    d = np.load(os.path.join(GOLDEN, "e2e_wifi648_qpsk_ofdm.npz"))
+    H = qc_expand(d["base"], int(d["Z"]))
+    bs, iters = int(d["batch_size"]), int(d["iters"])
+    for snr in d["snrs"]:
+        tag = f"snr{snr:g}".replace(".", "p")
+        llrs, out = d[f"llrs_{tag}"], d[f"out_{tag}"]
+        rows = (llrs.shape[0] // bs) * bs
+        assert llrs.dtype == np.float64 and out.dtype == np.float64 and not out[rows:].any()
+        r = oracle.sp_f32(H, llrs[:rows].astype(np.float32), iters, float(d["clamp"]))
+        assert np.array_equal(r["bits"].astype(np.float64), out[:rows])
+        assert (out[:rows] != d[f"codeword_{tag}"][:rows]).any()     # the waterfall: failing rows present
+
+
 def test_looped_reference_golden_settings():
     """The long-iteration goldens are the drop-in's / BASELINE configs' settings."""
     want = {"wifi648_12": (50, 192), "wifi1296_23": (20, 96), "wifi1944_56": (10, 48)}

@@ -33,11 +33,14 @@ What it records (all .npz, numeric arrays only — loadable with allow_pickle=Fa
   * e2e_wifi648_qpsk_ofdm.npz  the reference's whole receiver chain (bits, encode_bits, modulate_bits, gen_data's
                            32-point OFDM over AWGN, demodulate_signal) into decode_bits(llrs, H, 50, 40, 10) on
                            the (648,1/2) code, 96 rows per Es/N0 point (rows 80..95 stay 0) (e2e648).
+  * e2e_quantized.npz      the reference's quantized chain (3-bit ADC via gen_qdata, evaluate_quantized.py) into
+                           decode_bits at clamp 20: (64,32) at 3 iterations, (648,1/2) at 50; LLRs with exact
+                           zeros (e2eq).
   * bp_wifi648_12_sp_it50_cl20.npz  (648,1/2) 50 iterations at clamp 20, above the p-clamp ceiling; plus
                            (wificlampb32) the reference's .double() module with the fp32 module's p-clamp bound
                            swapped in at run time (f32_pclamp): p1_f64b32_* / z_f64b32_*.
 
-    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32] [wifi1944c2] [e2e648]
+    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32] [wifi1944c2] [e2e648] [e2eq]
 """
 import contextlib
 import os
@@ -488,6 +491,43 @@ def gen_e2e648():
                         batch_size=bs, clamp=clamp, ofdm_size=ofdm, snrs=np.array(snrs), **rec)
 
 
+def gen_e2e_quantized():
+    """e2e_quantized.npz: the reference's quantized receiver chain (evaluate_quantized.py:42-46,98,137): bits ->
+    encode_bits -> modulate_bits -> gen_data (32-point OFDM over AWGN) -> gen_qdata (ADC with AGC clip = std x
+    ratio, ofdm_functions.py:118-128) -> demodulate_signal LLRs -> decode_bits(qrx_llrs, H, iters, bs, 20).  The
+    LLRs contain exact zeros (s = +-0 in the first VC layer).  Two cases: the reference's own (64,32) with its
+    evaluator's 3-bit ADC, clip ratio 1 and 3 iterations; (648,1/2) with a 5-bit ADC, clip ratio 2, 50 iterations."""
+    from ldpc_amd.codes import get_code
+    rec = {}
+    cases = [("peg64", parity.H.astype(np.int64), np.asarray(parity.G, np.int64) if hasattr(parity, "G") else None,
+              3, 100, 32, 2.0, 3, 1), ("wifi648", None, None, 50, 96, 40, 2.0, 5, 2)]
+    for name, H, G, iters, B, bs, snrdb, qbits, clip_ratio in cases:
+        if H is None:
+            H = np.asarray(get_code("wifi648_12")[0], dtype=np.int64)
+        if G is None or G.shape[0] != H.shape[1]:
+            enc = Encoder(H)
+            G = enc.encode(np.eye(enc.k, dtype=np.int64)).T.astype(np.int64)
+        k = G.shape[1]
+        assert not ((H @ G) % 2).any()
+        np.random.seed(4242 + H.shape[1])
+        bits = OF.create_bits(B * k)
+        cbits = OF.encode_bits(bits, G)
+        tx = OF.modulate_bits(cbits)
+        rx_signal, _, _, _ = OF.gen_data(tx, snrdb, 32)
+        _, _, qrx_llrs = OF.gen_qdata(rx_signal, snrdb, qbits, clip_ratio, 32)
+        llrs = qrx_llrs.reshape((-1, H.shape[1]))
+        out = OF.decode_bits(llrs, H, iters, bs, 20)
+        rec[f"H_{name}"] = H.astype(np.uint8)
+        rec[f"llrs_{name}"] = llrs
+        rec[f"codeword_{name}"] = cbits.reshape((-1, H.shape[1])).astype(np.uint8)
+        rec[f"out_{name}"] = out
+        rec[f"cfg_{name}"] = np.array([iters, bs, 20, qbits, clip_ratio])
+        rows = (B // bs) * bs
+        print("e2eq", name, "zero LLRs:", int((llrs == 0).sum()), "distinct:", len(np.unique(llrs)),
+              "bit errors in decoded rows:", int((out[:rows] != rec[f"codeword_{name}"][:rows]).sum()), flush=True)
+    np.savez_compressed(os.path.join(HERE, "e2e_quantized.npz"), **rec)
+
+
 def gen_x0():
     """bp_x0.npz: the reference forward with NON-ZERO initial messages x (bp/bp.py:43-47), which the first
     layer consumes like any later one: (64,32) at iterations 0 / 1 / 5 and (648,1/2) at 3, clamp 10, x drawn
@@ -519,10 +559,10 @@ def gen_x0():
 
 if __name__ == "__main__":
     parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong", "wificlamp", "wificlampb32",
-                             "wifi1944c2", "e2e648"]
+                             "wifi1944c2", "e2e648", "e2eq"]
     for part in parts:
         {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp, "x0": gen_x0,
          "wifilong": gen_wifi_sp_long,
          "wificlamp": lambda: gen_wifi_sp_long(WIFI_SP_CLAMPS, clamp_tag=True),
-         "wificlampb32": gen_wifi_clamp_f32bound, "wifi1944c2": gen_wifi1944_c2, "e2e648": gen_e2e648}[part]()
+         "wificlampb32": gen_wifi_clamp_f32bound, "wifi1944c2": gen_wifi1944_c2, "e2e648": gen_e2e648, "e2eq": gen_e2e_quantized}[part]()
     print("done")

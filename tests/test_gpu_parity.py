@@ -581,6 +581,17 @@ def test_decode_bits_reference_receiver_chain_golden():
         assert np.array_equal(out, d[f"out_{tag}"]), tag
 
 
+def test_decode_bits_reference_quantized_chain_golden():
+    """The drop-in on the reference's quantized receiver chain (tests/golden/e2e_quantized.npz: gen_qdata's ADC,
+    evaluate_quantized.py's pipeline, clamp 20): (64,32) at 3 iterations with the evaluator's 3-bit ADC, (648,1/2)
+    at 50 with a 5-bit ADC — LLRs with exact zeros; the float64 output equals the reference's exactly."""
+    d = np.load(os.path.join(GOLDEN, "e2e_quantized.npz"))
+    for name in ("peg64", "wifi648"):
+        iters, bs, clamp = (int(x) for x in d[f"cfg_{name}"][:3])
+        out = ldpc_amd.decode_bits(d[f"llrs_{name}"], d[f"H_{name}"].astype(np.int64), iters, bs, clamp)
+        assert out.dtype == np.float64 and np.array_equal(out, d[f"out_{name}"]), name
+
+
 def test_decode_llr_sign_convention():
     """decode(..., llr_sign="p0/p1") takes the communications convention (positive = bit 0): the same bits
     as the reference convention on the negated input."""

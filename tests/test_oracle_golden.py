@@ -218,6 +218,23 @@ def test_oracle_reference_receiver_chain_golden():
         assert (out[:rows] != d[f"codeword_{tag}"][:rows]).any()     # the waterfall: failing rows present
 
 
+def test_oracle_reference_quantized_chain_golden():
+    """e2e_quantized.npz: the reference's quantized receiver chain (ADC via gen_qdata, evaluate_quantized.py) into
+    decode_bits at clamp 20 — (64,32) with the evaluator's 3-bit ADC at 3 iterations, (648,1/2) with a 5-bit ADC at
+    50; LLRs with exact zeros.  Both oracle forms (the reference's fp32 operations and the (D, S) form) give the
+    reference's bits on every decoded row, failures included."""
+    d = np.load(os.path.join(GOLDEN, "e2e_quantized.npz"))
+    for name in ("peg64", "wifi648"):
+        H = d[f"H_{name}"].astype(np.int64)
+        llrs, out = d[f"llrs_{name}"], d[f"out_{name}"]
+        iters, bs, clamp = (int(x) for x in d[f"cfg_{name}"][:3])
+        rows = (llrs.shape[0] // bs) * bs
+        assert (llrs == 0).any() and not out[rows:].any()
+        for stable in (False, True):
+            r = oracle.sp_f32(H, llrs[:rows].astype(np.float32), iters, float(clamp), stable=stable)
+            assert np.array_equal(r["bits"].astype(np.float64), out[:rows]), (name, stable)
+
+
 def test_looped_reference_golden_settings():
     """The long-iteration goldens are the drop-in's / BASELINE configs' settings."""
     want = {"wifi648_12": (50, 192), "wifi1296_23": (20, 96), "wifi1944_56": (10, 48)}

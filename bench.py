@@ -7,8 +7,12 @@ Before timing, one untimed pass over all 11 points produces the BER/BLER curve (
 summed over ranks with an RCCL all-reduce — the only collective; the codeword batches shard with no
 data-path exchange, so scaling is weak).
 
-    python bench.py [--gpus N --steps K --warmup W]                  # N=1
-    torchrun --nproc-per-node N ... bench.py --gpus N ...            # one rank per GPU
+    python bench.py [--gpus N --steps K --warmup W]                  # N ranks, one GPU each (started here)
+    torchrun --nproc-per-node N ... bench.py --gpus N ...            # the same under a launcher
+
+--gpus N is authoritative: without launcher variables, N > 1 starts N fresh rank processes of this script
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, RCCL) before this process touches a GPU, streams rank 0's
+line and exits with the worst rank's code; under a launcher, WORLD_SIZE must equal N.
 
 The other BASELINE.json configs run as short legs of the same script after the headline, reported under
 ``side.configs`` (never ``value``), each event-timed over two launches per Eb/N0 point with its own
@@ -32,6 +36,19 @@ sys.path.insert(0, os.path.join(ROOT, "ldpc-sims_amd"))
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def _dist_module():
+    """ldpc_amd/dist.py loaded on its own: the launcher must not import the package (which loads the HIP
+    library) before it has decided whether this process decodes or only starts the rank processes."""
+    import importlib.util
+    name = "_ldpc_amd_dist_launcher"
+    if name not in sys.modules:
+        spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "ldpc-sims_amd", "ldpc_amd", "dist.py"))
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+    return sys.modules[name]
 
 
 def algorithmic_bytes_per_cw(n, E, iters, s_m=4, s_l=4):
@@ -70,6 +87,19 @@ def main():
     ap.add_argument("--counters-json", default=os.path.join(ROOT, "profiles", "counters.json"),
                     help="per-launch PMC counts per configuration (scripts/gpu_profile.sh + counters_summary.py)")
     args = ap.parse_args()
+
+    # --gpus N is authoritative: under a launcher (torchrun) WORLD_SIZE must equal N; without one, N > 1
+    # starts N fresh rank processes of this script (one GPU each, RCCL) before this process touches a GPU
+    launcher = _dist_module()
+    spawn = launcher.resolve_world(args.gpus)
+    if spawn is not None and spawn > 1:
+        if not os.environ.get("LDPC_BENCH_SHARE_GPU"):
+            import torch  # device_count() does not initialise the GPU (this process only starts children)
+            have = torch.cuda.device_count()
+            if have < spawn:
+                raise SystemExit(f"--gpus {spawn} but only {have} GPU(s) visible")
+        log(f"bench: starting {spawn} rank processes")
+        sys.exit(launcher.spawn_ranks([os.path.abspath(__file__), *sys.argv[1:]], spawn))
 
     import torch
     import torch.distributed as dist

@@ -91,9 +91,11 @@ int ldpc_workspace_size(const ldpc_graph* g, int64_t B, const ldpc_params* p, si
 int ldpc_decode_ex(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_params* p, uint8_t* bits_out,
                    void* soft_out, int32_t* iters_used, void* workspace, size_t workspace_bytes, void* stream);
 
-/* Convenience form (float llr, internal workspace). */
+/* Convenience form (float llr, internal workspace, alpha 1 / beta 0 / qmax 15 / app_max 127 / qstep 1) —
+ * the signature SURVEY.md §8(b) sketches: iters_used[B] (may be NULL) as in ldpc_decode_ex.  Replaces the
+ * same reference interface (bp/bp.py:43-51, ofdm/ofdm_functions.py:152-161); LDPC_F_F64 is ignored. */
 int ldpc_decode(const ldpc_graph* g, const float* llr, int64_t B, int32_t iters, float clamp, int32_t algo,
-                int32_t flags, uint8_t* bits_out, float* soft_out, void* stream);
+                int32_t flags, uint8_t* bits_out, float* soft_out, int32_t* iters_used, void* stream);
 
 /* Weighted BP — the reference module with trained (non-unit) VC weights: layers[i][0].input_weight
  * (E x E, masked by mask_v) and llr_weight (1 x n) per iteration, final_layer[0].input_weight (n x E) and

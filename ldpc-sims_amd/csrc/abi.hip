@@ -500,7 +500,7 @@ int ldpc_decode_x0(const ldpc_graph* g, const void* llr, int64_t B, const ldpc_p
 }
 
 int ldpc_decode(const ldpc_graph* g, const float* llr, int64_t B, int32_t iters, float clamp, int32_t algo,
-                int32_t flags, uint8_t* bits_out, float* soft_out, void* stream) {
+                int32_t flags, uint8_t* bits_out, float* soft_out, int32_t* iters_used, void* stream) {
     ldpc_params p{};
     p.iters = iters;
     p.algo = algo;
@@ -511,7 +511,7 @@ int ldpc_decode(const ldpc_graph* g, const float* llr, int64_t B, int32_t iters,
     p.qmax = 15;
     p.app_max = 127;
     p.qstep = 1.0f;
-    return ldpc_decode_ex(g, llr, B, &p, bits_out, soft_out, nullptr, nullptr, 0, stream);
+    return ldpc_decode_ex(g, llr, B, &p, bits_out, soft_out, iters_used, nullptr, 0, stream);
 }
 
 int ldpc_decode_bits_host(const ldpc_graph* gc, const double* llr, int64_t rows, const ldpc_params* p, double* out,

@@ -74,7 +74,7 @@ def load(path: str | None = None):
     L.ldpc_graph_info.argtypes = [vp, vp, vp, vp, vp]
     L.ldpc_workspace_size.argtypes = [vp, i64, ctypes.POINTER(Params), ctypes.POINTER(sz)]
     L.ldpc_decode_ex.argtypes = [vp, vp, i64, ctypes.POINTER(Params), vp, vp, vp, vp, sz, vp]
-    L.ldpc_decode.argtypes = [vp, vp, i64, i32, ctypes.c_float, i32, i32, vp, vp, vp]
+    L.ldpc_decode.argtypes = [vp, vp, i64, i32, ctypes.c_float, i32, i32, vp, vp, vp, vp]
     L.ldpc_count_errors.argtypes = [vp, vp, i64, i32, i32, vp, vp]
     L.ldpc_awgn_llr.argtypes = [vp, vp, i64, i32, ctypes.c_float, ctypes.c_uint64, i64, vp]
     L.ldpc_random_bits.argtypes = [vp, i64, i32, ctypes.c_uint64, i64, vp]
@@ -94,9 +94,26 @@ def load(path: str | None = None):
         getattr(L, f).restype = ctypes.c_int
     L.ldpc_last_error.restype = ctypes.c_char_p
     L.ldpc_version.restype = ctypes.c_char_p
+    L._ldpc_path = p
     if path is None:
         _lib = L
     return L
+
+
+_digests: dict = {}
+
+
+def library_digest(path: str | None = None) -> str:
+    """sha1 of the library file in use (the build identity: every kernel change rebuilds it)."""
+    import hashlib
+    p = path or load()._ldpc_path
+    if p not in _digests:
+        h = hashlib.sha1()
+        with open(p, "rb") as f:
+            for blk in iter(lambda: f.read(1 << 20), b""):
+                h.update(blk)
+        _digests[p] = h.hexdigest()
+    return _digests[p]
 
 
 def check(rc: int):

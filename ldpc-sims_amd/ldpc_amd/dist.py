@@ -12,6 +12,11 @@ bits).  No data-path collective exists because decoding never exchanges messages
 """
 from __future__ import annotations
 
+import os
+import socket
+import subprocess
+import sys
+import time
 from dataclasses import dataclass
 from typing import Callable, Sequence
 
@@ -76,6 +81,80 @@ def max_over_ranks(value: float, device="cpu", group=None) -> float:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         return float(t.item())
     return value
+
+
+RANK_VARS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def resolve_world(requested: int, env=None) -> int | None:
+    """How a ``--gpus N`` entry point runs.  Returns None when this process is one rank of an existing
+    launch (``WORLD_SIZE`` set, e.g. by torchrun or by ``spawn_ranks``) — then ``WORLD_SIZE`` must equal
+    ``N`` or this raises ``SystemExit`` (a torchrun with a different rank count is a mislabelled run);
+    otherwise returns N, the number of rank processes this process must start (1 = run in-process)."""
+    env = os.environ if env is None else env
+    if requested < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {requested})")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != requested:
+            raise SystemExit(f"WORLD_SIZE={ws} from the launcher but --gpus {requested}: refusing a run whose "
+                             "rank count differs from the one it would report")
+        return None
+    return requested
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(argv: Sequence[str], world: int, env=None, poll_s: float = 0.2) -> int:
+    """Start ``world`` fresh child processes ``python <argv>`` — one rank per GPU, the environment torchrun
+    would give them (RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE, MASTER_ADDR 127.0.0.1 and a free
+    port) — and wait for them.  The children inherit stdout / stderr, so rank 0's JSON line and every
+    rank's progress stream through unchanged.  The caller must not have touched the GPU (it starts
+    children, it never execs).  If any rank fails, the others are terminated (they would wait forever in
+    a collective) and the worst return code is returned.
+
+    This replaces the reference's single-process ``nn.DataParallel`` mode (ofdm_functions.py:141-145) with
+    one process per GPU, so ``bench.py --gpus N`` runs N ranks without an external launcher."""
+    env = dict(os.environ if env is None else env)
+    for k in RANK_VARS:
+        env.pop(k, None)
+    port = _free_port()
+    procs = []
+    first = []   # return codes of the ranks that failed on their own (before any was terminated here)
+    try:
+        for r in range(world):
+            e = dict(env, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                     MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, *argv], env=e))
+        while True:
+            rcs = [p.poll() for p in procs]
+            first = [rc for rc in rcs if rc not in (None, 0)]
+            if first or all(rc is not None for rc in rcs):
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    rcs = [p.returncode for p in procs]
+    bad = first or [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"spawn_ranks: rank return codes {rcs}", file=sys.stderr, flush=True)
+        # a signal-killed child reports -signum: the shell's 128 + signum
+        return max((128 - rc if rc < 0 else rc) for rc in bad)
+    return 0
 
 
 def sweep(points: Sequence[float], total_codewords: int, rate: float, info_bits: int,

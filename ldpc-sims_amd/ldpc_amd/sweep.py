@@ -14,6 +14,7 @@ given) every finished point's world-summed counters are appended as one JSON lin
 configuration, and a restarted sweep with the same configuration skips the points already recorded.
 
     python -m ldpc_amd.sweep --code peg64_32 --algo tanh --iters 3 --clamp 20 --snr 0:1:10 --n 65536
+    python -m ldpc_amd.sweep --gpus 8 ...                    # 8 rank processes, one GPU each (or torchrun)
     torchrun --nproc-per-node 8 -m ldpc_amd.sweep ...        # shards codewords; one RCCL all-reduce
 """
 from __future__ import annotations
@@ -22,6 +23,7 @@ import argparse
 import json
 import os
 import pickle
+import sys
 import time
 
 import numpy as np
@@ -32,6 +34,19 @@ from .codes import get_code
 from .channel import adc_quantize, ofdm_demod, ofdm_tx
 from .synth import DeviceEncoder
 from .dist import ebn0_sigma, shard_bounds
+
+
+def code_digest(H) -> str:
+    """sha1 over H's shape and its nonzeros in check-major CSR order — the identity of a parity-check
+    matrix, whatever its container (dense 0/1 array or SparseCode)."""
+    import hashlib
+    from .codes import Graph
+    g = Graph.from_H(H)
+    h = hashlib.sha1()
+    h.update(np.asarray([g.m, g.n], np.int64).tobytes())
+    h.update(np.ascontiguousarray(g.row_ptr, np.int32).tobytes())
+    h.update(np.ascontiguousarray(g.col_idx, np.int32).tobytes())
+    return h.hexdigest()
 
 
 def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=0.0, snr_db=(0.0,),
@@ -50,9 +65,10 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
     unquantized ones.
 
     ``checkpoint``: a JSON-lines file of finished points (see the module docstring): points recorded there
-    for this exact configuration (every argument that shapes the data or the decode, the point's index and
-    value, the world size) are taken from it instead of being decoded again; rank 0 appends each newly
-    finished point as soon as its counters are summed over the ranks."""
+    for this exact configuration (every argument that shapes the data or the decode, a digest of H, a
+    digest of the decoder library, the point's index and value, the world size) are taken from it instead
+    of being decoded again; rank 0 appends each newly finished point as soon as its counters are summed
+    over the ranks.  Ranks without a process group (world > 1 given by hand) use ``<checkpoint>.rank<r>``."""
     import torch
     H, _ = get_code(code) if isinstance(code, str) else (code, None)
     m, n = H.shape
@@ -118,10 +134,15 @@ def run(code="wifi648_12", algo="minsum", iters=50, clamp=20.0, alpha=1.0, beta=
     # counters summed over ranks only inside a process group; without one (tests: rank/world given by hand)
     # each rank keeps its own shard's counts, and its checkpoint records are its own (rank in the key)
     reduced = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-    fp = dict(config, qstep=qstep, qmax=qmax, app_max=app_max, ofdm_size=ofdm_size, codewords=codewords,
-              batch=batch, seed=seed, world=world, snr_db=[float(x) for x in snr_db])
+    # the key names H itself (a digest of its shape and nonzeros: two custom matrices never share points) and
+    # the decoder build (a digest of the loaded library: a rebuilt decoder never resumes old arithmetic)
+    fp = dict(config, h_digest=code_digest(H), library=_abi.library_digest(), qstep=qstep, qmax=qmax,
+              app_max=app_max, ofdm_size=ofdm_size, codewords=codewords, batch=batch, seed=seed, world=world,
+              snr_db=[float(x) for x in snr_db])
     if not reduced and world > 1:
         fp["rank"] = rank
+        if checkpoint:  # ranks outside a process group write at once: each gets a file of its own
+            checkpoint = f"{checkpoint}.rank{rank}"
     P = len(snr_db)
     cnt = torch.zeros((P, 3), dtype=torch.int64, device=dev)
     # points finished by an earlier run of this configuration: rank 0 reads the checkpoint, the others learn
@@ -262,7 +283,18 @@ def main(argv=None):
     ap.add_argument("--out", default=None, help="results .json or .pkl (reference schema)")
     ap.add_argument("--checkpoint", default=None,
                     help="per-point resume file (JSON lines); default <out>.points.jsonl when --out is given")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each); N > 1 without a launcher starts N rank processes itself")
     a = ap.parse_args(argv)
+    if a.gpus is not None:
+        from .dist import resolve_world, spawn_ranks
+        spawn = resolve_world(a.gpus)
+        if spawn is not None and spawn > 1:
+            pkg_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+            env = dict(os.environ, PYTHONPATH=os.pathsep.join(
+                x for x in (pkg_root, os.environ.get("PYTHONPATH")) if x))
+            args = list(sys.argv[1:] if argv is None else argv)
+            raise SystemExit(spawn_ranks(["-m", "ldpc_amd.sweep", *args], spawn, env=env))
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))

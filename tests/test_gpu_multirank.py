@@ -71,16 +71,46 @@ def test_bench_two_ranks_equal_one_process_over_both_shards():
     assert 0 < one["ber"]["coded_bler"][0] < 1   # a point with errors, so equal counts mean something
 
 
+def test_bench_gpus2_starts_its_own_ranks():
+    """``python bench.py --gpus 2`` with NO launcher variables (the driver's plain invocation): bench.py
+    starts the two rank processes itself (ldpc_amd.dist.spawn_ranks) before touching the GPU; the line
+    reports 2 GPUs, the process group saw world size 2, and the counts equal one process over both shards.
+    (Shared-GPU / gloo rehearsal switches only because this box has one GPU.)"""
+    common = ["bench.py", "--steps", "2", "--warmup", "1", "--iters", "10", "--ebn0", "1:1:3",
+              "--no-cpu-baseline", "--no-legs"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                                                              "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(LDPC_BENCH_SHARE_GPU="1", LDPC_BENCH_BACKEND="gloo", PYTHONPATH=os.path.join(ROOT, "ldpc-sims_amd"))
+    p = subprocess.run([sys.executable, *common, "--gpus", "2", "--batch", "4096"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1                                   # rank 0's line only
+    two = json.loads(lines[0])
+    one = _bench_line(_launch([*common, "--gpus", "1", "--batch", "8192"], 1))
+    assert two["n_gpus"] == 2 and two["ranks"]["world_size"] == 2 and two["config"]["global_batch"] == 8192
+    assert [r["rank"] for r in two["ranks"]["per_rank"]] == [0, 1]
+    assert two["ber"] == one["ber"]
+
+
 def test_sweep_two_ranks_equal_one_process(tmp_path):
     common = ["-m", "ldpc_amd.sweep", "--code", "wifi648_12", "--algo", "minsum", "--iters", "10",
               "--snr", "1:1:3", "--n", "10000", "--batch", "3000", "--seed", "4"]
     _launch([*common, "--out", str(tmp_path / "two.json")], 2)
     _launch([*common, "--out", str(tmp_path / "one.json")], 1)
+    # --gpus 2 without launcher variables: the sweep starts its own two ranks
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                                                              "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(LDPC_BENCH_SHARE_GPU="1", LDPC_BENCH_BACKEND="gloo", PYTHONPATH=os.path.join(ROOT, "ldpc-sims_amd"))
+    p = subprocess.run([sys.executable, *common, "--gpus", "2", "--out", str(tmp_path / "own.json")], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
     two = json.load(open(tmp_path / "two.json"))
     one = json.load(open(tmp_path / "one.json"))
-    assert two["codewords"] == one["codewords"] == [10000] * 3
+    own = json.load(open(tmp_path / "own.json"))
+    assert two["codewords"] == one["codewords"] == own["codewords"] == [10000] * 3
     for key in ("uncoded_ber", "coded_ber", "coded_bler"):
-        assert two[key] == one[key], key
+        assert two[key] == one[key] == own[key], key
 
 
 def test_bench_dvbs2_config4_two_ranks_equal_one_process():

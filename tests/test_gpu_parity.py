@@ -96,6 +96,43 @@ def test_decode_bits_host_pipeline_chunks(chunk):
             == _abi.LDPC_EINVAL
 
 
+def test_ldpc_decode_short_form_with_iters_used():
+    """ldpc_decode (the SURVEY §8(b) signature, host pointers, internal workspace) against the reference's
+    golden bits and against ldpc_decode_ex: same bits, p1 bitwise, and iters_used filled — the fixed count
+    without early stop, the per-codeword counts of ldpc_decode_ex with LDPC_F_EARLY_STOP."""
+    import ctypes
+    d = np.load(os.path.join(GOLDEN, "decode_bits_peg64.npz"))
+    H = d["H"]
+    dec = ldpc_amd.get_decoder(H)
+    x = np.ascontiguousarray(d["llrs"], np.float32)
+    B, n = x.shape
+    it, cl = int(d["iters"]), float(d["clamp"])
+    for flags in (0, _abi.F_EARLY_STOP):
+        bits = np.empty((B, n), np.uint8)
+        p1 = np.empty((B, n), np.float32)
+        used = np.full(B, -1, np.int32)
+        _abi.check(dec.lib.ldpc_decode(dec._h, x.ctypes.data, B, it, cl, _abi.ALGO_TANH_SP, flags, bits.ctypes.data,
+                                       p1.ctypes.data, used.ctypes.data, None))
+        p = dec.params(it, "tanh", cl, early_stop=bool(flags))
+        bits2 = np.empty_like(bits)
+        p12 = np.empty_like(p1)
+        used2 = np.full(B, -2, np.int32)
+        _abi.check(dec.lib.ldpc_decode_ex(dec._h, x.ctypes.data, B, ctypes.byref(p), bits2.ctypes.data,
+                                          p12.ctypes.data, used2.ctypes.data, None, 0, None))
+        assert np.array_equal(bits, bits2) and np.array_equal(p1.view(np.uint32), p12.view(np.uint32))
+        assert np.array_equal(used, used2)
+        if flags == 0:
+            assert (used == it).all()
+            rows = (B // int(d["batch_size"])) * int(d["batch_size"])
+            assert np.array_equal(bits[:rows].astype(np.float64), d["out"][:rows])
+        else:
+            assert (used >= 0).all() and (used <= it).all() and used.min() < it
+    # NULL iters_used and NULL soft are allowed
+    bits = np.empty((B, n), np.uint8)
+    _abi.check(dec.lib.ldpc_decode(dec._h, x.ctypes.data, B, it, cl, _abi.ALGO_TANH_SP, 0, bits.ctypes.data, None,
+                                   None, None))
+
+
 def test_decode_bits_wifi648_equals_device_path():
     """The drop-in over a multi-chunk (648,1/2) batch equals the device-pointer decode bit for bit."""
     import ctypes

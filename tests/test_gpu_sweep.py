@@ -8,6 +8,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
+from ldpc_amd.codes import get_code  # noqa: E402
 from ldpc_amd.sweep import run  # noqa: E402
 from softparity import _log  # noqa: E402
 
@@ -147,3 +148,29 @@ def test_sweep_resumes_per_point(tmp_path):
     for key in ("uncoded_ber", "coded_ber", "coded_bler", "codewords"):
         assert np.array_equal(np.asarray(again[key]), np.asarray(full[key])), key
     assert 0 < full["coded_bler"][0] < 1
+
+
+def test_sweep_checkpoint_keys_h_and_library(tmp_path):
+    """The checkpoint key names H itself and the decoder build: a second CUSTOM matrix with the same settings
+    and file resumes nothing from the first (both are 'custom' by name), and a record written by another
+    library build is ignored (the key once held only the name 'custom')."""
+    import json
+    from ldpc_amd import _abi
+    from ldpc_amd.sweep import code_digest
+    H = get_code("peg64_32")[0]
+    H2 = H[::-1].copy()                         # another matrix of the same shape (rows reversed)
+    assert code_digest(H) != code_digest(H2) and code_digest(H) == code_digest(H.copy())
+    ck = str(tmp_path / "pts.jsonl")
+    args = dict(snr_db=[2.0, 3.0], codewords=2000, batch=1024, seed=3)
+    a = run(H, "tanh", 3, 20.0, checkpoint=ck, **args)
+    recs = [json.loads(x) for x in open(ck)]
+    assert a["resumed_points"] == [] and recs[0]["config"]["code"] == "custom"
+    assert recs[0]["config"]["library"] == _abi.library_digest()
+    b = run(H2, "tanh", 3, 20.0, checkpoint=ck, **args)
+    assert b["resumed_points"] == []            # same settings, other H: nothing reused
+    assert run(H, "tanh", 3, 20.0, checkpoint=ck, **args)["resumed_points"] == [0, 1]
+    stale = [dict(r, config=dict(r["config"], library="0" * 40)) for r in recs]
+    ck2 = str(tmp_path / "stale.jsonl")
+    with open(ck2, "w") as f:
+        f.writelines(json.dumps(r) + "\n" for r in stale)
+    assert run(H, "tanh", 3, 20.0, checkpoint=ck2, **args)["resumed_points"] == []

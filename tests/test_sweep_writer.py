@@ -31,3 +31,22 @@ def test_pkl_has_every_key_plots_reads(tmp_path):
         assert np.isnan(d["coded_ber_quantized"]).all() != adc
         assert np.array_equal(d["coded_ber"], np.ones(4) * 0.01)
     save(_result(), str(tmp_path / "r.json"))
+
+
+def test_checkpoint_key_digests():
+    """The sweep checkpoint key's identities: H's digest depends on H's nonzeros and shape, not on
+    its container; the library digest is the sha1 of the loaded file."""
+    import hashlib
+    from ldpc_amd import _abi
+    from ldpc_amd.codes import get_code
+    from ldpc_amd.sweep import code_digest
+    H = get_code("peg64_32")[0]
+    assert code_digest(H) == code_digest(H.astype(np.int64)) == code_digest(H.copy())
+    assert code_digest(H) != code_digest(H[::-1].copy())
+    H3 = H.copy()
+    H3[0, np.flatnonzero(H3[0] == 0)[0]] = 1                 # one more edge
+    assert code_digest(H3) != code_digest(H)
+    dv = get_code("dvbs2_12")[0]                               # SparseCode container
+    assert len(code_digest(dv)) == 40
+    with open(_abi.load()._ldpc_path, "rb") as f:
+        assert _abi.library_digest() == hashlib.sha1(f.read()).hexdigest()

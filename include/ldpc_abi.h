@@ -73,6 +73,13 @@ int ldpc_graph_destroy(ldpc_graph* g);
  * specialised kernel in use (0 = generic CSR kernels). */
 int ldpc_graph_info(const ldpc_graph* g, int32_t* m, int32_t* n, int32_t* nnz, int32_t* qc_z);
 
+/* The kernel family a decode with these params runs on this graph: "qc-z<Z>" (register-resident
+ * quasi-cyclic kernels, 802.11n), "ira-z360" (DVB-S2-structured IRA codes, min-sum, fixed iterations) or
+ * "generic-csr" (any H).  Introspection only (benchmarks label their records with it); NULL on bad
+ * arguments.  The string is thread-local and valid until the next call on this thread.  No reference
+ * counterpart: the reference has one code path (dense masks, bp/masking.py). */
+const char* ldpc_kernel_path(const ldpc_graph* g, const ldpc_params* p);
+
 /* Device bytes ldpc_decode_ex needs as caller-provided workspace for a batch of B codewords. */
 int ldpc_workspace_size(const ldpc_graph* g, int64_t B, const ldpc_params* p, size_t* bytes);
 

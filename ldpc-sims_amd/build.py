@@ -17,7 +17,7 @@ SRCS = [("abi.hip", "abi.hip.o", []), ("generic.hip", "generic.hip.o", [])] + [
     ("generic_run.hip", f"generic_run_{n}.o", [f"-DRUN_T={t}", f"-DRUN_MS={ms}", f"-DRUN_ES={es}", f"-DRUN_NAME=generic_run_{n}"])
     for (n, t, ms, es) in _RUNS] + [("qc.hip", "qc.hip.o", []), ("qc_sl.hip", "qc_sl.hip.o", []), ("qc_pk.hip", "qc_pk.hip.o", []),
            ("qc_sl_es.hip", "qc_sl_es.hip.o", []), ("qc_es.hip", "qc_es.hip.o", []),
-           ("channel.hip", "channel.hip.o", [])]
+           ("channel.hip", "channel.hip.o", []), ("ira.hip", "ira.hip.o", [])]
 OUT = os.path.join(HERE, "ldpc_amd", "libldpc_hip.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off",  # min-sum must round exactly like oracle/ldpc_oracle.c (no FMA contraction)

@@ -25,6 +25,7 @@ struct ldpc_graph {
     int32_t* d_wofs = nullptr;  // weighted BP: [n+1] offsets of the per-variable d x d weight blocks
     int64_t W = 0;
     const ldpc::QCSpec* qc = nullptr;
+    ldpc::IRASpec* ira = nullptr;  // DVB-S2-structured IRA code (ira.hip), when not QC
     std::mutex mtx;  // guards the internal workspace
     void* ws = nullptr;
     size_t ws_bytes = 0;
@@ -178,11 +179,16 @@ static bool use_qc(const ldpc_graph* g, const ldpc_params* p) {
     return g->qc && !(p->flags & LDPC_F_FORCE_GENERIC) && qc_supports(g->qc, *p);
 }
 
+static bool use_ira(const ldpc_graph* g, const ldpc_params* p) {
+    return g->ira && !(p->flags & LDPC_F_FORCE_GENERIC) && ira_supports(g->ira, *p);
+}
+
 static size_t elem_size(const ldpc_params* p) { return (p->flags & LDPC_F_F64) ? 8 : 4; }
 
 // Workspace = kernel scratch followed (host-pointer callers only) by staging for llr/bits/soft/used.
 static size_t kernel_ws(const ldpc_graph* g, int64_t B, const ldpc_params* p) {
     if (use_qc(g, p)) return align256(qc_workspace(g->qc, B, *p));
+    if (use_ira(g, p)) return align256(ira_workspace(g->ira, B, *p));
     return align256(generic_workspace(gargs(g), B, *p));
 }
 static size_t staging_ws(const ldpc_graph* g, int64_t B, const ldpc_params* p) {
@@ -341,6 +347,7 @@ int ldpc_graph_create(int32_t m, int32_t n, int32_t nnz, const int32_t* row_ptr,
         return rc;
     }
     g->qc = detect_qc(m, n, rp, ci);
+    if (!g->qc) g->ira = ira_detect(m, n, rp.data(), ci.data(), device);
     *out = g;
     return LDPC_OK;
 }
@@ -369,6 +376,7 @@ int ldpc_graph_destroy(ldpc_graph* g) {
     (void)hipFree(g->d_var_ptr);
     (void)hipFree(g->d_var_edges);
     (void)hipFree(g->d_wofs);
+    ira_free(g->ira);
     if (g->ws) (void)hipFree(g->ws);
     pipe_free(g);
     delete g;
@@ -382,6 +390,18 @@ int ldpc_graph_info(const ldpc_graph* g, int32_t* m, int32_t* n, int32_t* nnz, i
     if (nnz) *nnz = g->E;
     if (z) *z = g->qc ? qc_z(g->qc) : 0;
     return LDPC_OK;
+}
+
+const char* ldpc_kernel_path(const ldpc_graph* g, const ldpc_params* p) {
+    static thread_local std::string path;
+    if (!g || !params_valid(p)) {
+        set_error(LDPC_EINVAL, "bad kernel_path query");
+        return nullptr;
+    }
+    if (use_qc(g, p)) path = "qc-z" + std::to_string(qc_z(g->qc));
+    else if (use_ira(g, p)) path = "ira-z360";
+    else path = "generic-csr";
+    return path.c_str();
 }
 
 int ldpc_workspace_size(const ldpc_graph* g, int64_t B, const ldpc_params* p, size_t* bytes) {
@@ -443,6 +463,8 @@ static int decode_impl(const ldpc_graph* gc, const void* llr, int64_t B, const l
     int rc;
     if (use_qc(g, p)) {
         rc = qc_decode(g->qc, llr_d, B, *p, bits_d, soft_d, used_d, ws, st);
+    } else if (use_ira(g, p) && !w) {
+        rc = ira_decode(g->ira, (const float*)llr_d, B, *p, bits_d, (float*)soft_d, used_d, ws, st);
     } else {
         rc = generic_decode(gargs(g), llr_d, B, *p, bits_d, soft_d, used_d, ws, st, w);
     }

@@ -430,4 +430,13 @@ bool qc_supports(const QCSpec* s, const ldpc_params& p);
 size_t qc_workspace(const QCSpec* s, int64_t B, const ldpc_params& p);
 int qc_decode(const QCSpec* s, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
               int32_t* iters_used, char* ws, hipStream_t st);
+
+// IRA codes with the DVB-S2 structure (Z = 360), min-sum (ira.hip)
+struct IRASpec;
+IRASpec* ira_detect(int m, int n, const int32_t* row_ptr, const int32_t* col_idx, int device);
+void ira_free(IRASpec* s);
+bool ira_supports(const IRASpec* s, const ldpc_params& p);
+size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params& p);
+int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params& p, uint8_t* bits, float* soft,
+               int32_t* iters_used, char* ws, hipStream_t st);
 }  // namespace ldpc

@@ -1,0 +1,430 @@
+// ira.hip — min-sum decoder for IRA codes with the DVB-S2 structure (EN 302 307 §5.3.2: information bit m of
+// group g is accumulated into parity addresses (x + m q) mod M for every x of the group's table row; parity
+// staircase p_j ^= p_{j-1}), BASELINE config [4]: DVB-S2 64800 rate 1/2, 50 min-sum iterations.
+//
+// Why a kernel of its own.  The generic CSR kernels (generic_impl.h) stream every message through HBM each
+// iteration — 16E + 4n bytes per codeword-iteration, 3.89 MB for DVB-S2 — and run at 0.85 of the chip's
+// streaming rate: the byte count is the bound.  Relabelling check j = a + q b as (row a, position b) turns the
+// code into a quasi-cyclic one with Z = 360: information edge (g, t) with table address x_t connects variable
+// (g, m) to check (a_t, (s_t + m) mod 360), a_t = x_t mod q, s_t = x_t div q; the staircase connects parity
+// (a, b) to checks (a, b) and its successor.  Lanes run over the 360 positions of one row of ONE codeword, so
+// every access is a contiguous row segment (with one wrap) of a codeword-local array, whatever the batch.
+//
+// Dataflow (flooding, the oracle's operation order — oracle/numpy_ref.py ms, oracle/ldpc_oracle.c ms_f32):
+//   check state  per check: mag1, mag2 (the two output magnitudes after ms_mag), meta = argmin slot (bits
+//                27..31) | sign bit of every slot's c2v (bit s) — the exact c2v of every edge in 12 bytes
+//   k_ira_vn     app_v = L_v + sum of v's c2v in ASCENDING CHECK order (decompressed from the check states)
+//   k_ira_cn     v2c = app_v - c2v_old (decompressed from its own state), two-minimum, new state
+// which are the oracle's VN (app = L + sum x_k; v2c = app - x_k) and CN bit for bit: the CN's order statistics
+// and sign XOR do not depend on the slot order (an argmin tie has min2 == min1, so either slot gets the same
+// magnitude), and the VN sums in the oracle's order — for an information variable the ascending check order
+// of its d edges is the x-sorted table row rotated by the number of edges whose position wraps (b = s_t + m
+// >= 360 gives the smaller check index), a per-lane barrel rotation.
+// Bytes per codeword-iteration beyond L2 (each codeword's tasks run on one XCD back to back, so the
+// re-reads of its check states and posteriors hit L2): L (4n) + states (12M) + app (4n) in the VN, app (4n)
+// + states read and written (24M) in the CN = 16n + 36M = 2.1 MB for DVB-S2 1/2, against 3.89 MB for the
+// two-array dataflow.  A chunk of codewords whose arrays (8n + 12M bytes each) fit the Infinity Cache
+// decodes all its iterations before the next chunk starts.
+#include <stdlib.h>
+
+#include <algorithm>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+
+namespace ldpc {
+
+constexpr int kIZ = 360;       // DVB-S2 lifting (normal and short frames)
+constexpr int kIVS = 16;       // table stride: information-variable degree bound
+constexpr int kICS = 24;       // table stride: information slots per check bound
+constexpr int kIPS = 24;       // parity slots: kIPS (p_j) and kIPS + 1 (p_{j-1}); meta bits 0..25, argmin 27..31
+
+struct IRASpec {
+    int q = 0, G = 0, k = 0, n = 0, M = 0, E = 0, maxdv = 0, maxr = 0, device = 0;
+    int32_t *vn = nullptr, *vdeg = nullptr, *cn = nullptr, *cdeg = nullptr;  // device tables
+};
+
+struct IRADev {
+    const int32_t *vn, *vdeg, *cn, *cdeg;
+    int q, G, k, n, M;
+};
+
+// c2v of slot `slot` from a check state: the argmin slot gets mag2, every other mag1; sign bit from meta
+__device__ __forceinline__ float ira_c2v(float2 st, uint32_t mt, int slot) {
+    const float mag = ((mt >> 27) == (uint32_t)slot) ? st.y : st.x;
+    return u2f(f2u(mag) | ((mt << (31 - slot)) & 0x80000000u));
+}
+
+// Workgroup b -> (codeword, task): blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch),
+// so the T tasks of a codeword get consecutive blocks of one XCD and its arrays stay in that XCD's L2 while
+// its tasks run.  A speed choice only: any placement gives the same results.
+__device__ __forceinline__ bool ira_task(int T, int Bc, int& cw, int& task) {
+    const int b = blockIdx.x;
+    const int kk = b >> 3;
+    const int c = kk / T;
+    cw = c * 8 + (b & 7);
+    task = kk - c * T;
+    return cw < Bc;
+}
+
+// c'[i] = c[(i + rho) mod D], rho < D, by log2(D) stages of selects (rotations compose additively mod D)
+template <int D>
+__device__ __forceinline__ void rotate_left(float (&c)[D], int rho) {
+    static_for<0, 5>([&](auto BB) __attribute__((always_inline)) {
+        constexpr int sh = 1 << decltype(BB)::value;
+        if constexpr (sh < D) {
+            const bool on = (rho & sh) != 0;
+            float t[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) t[i] = on ? c[(i + sh) % D] : c[i];
+#pragma unroll
+            for (int i = 0; i < D; ++i) c[i] = t[i];
+        }
+    });
+}
+
+// app of information variable (g, pos) of degree D: L + its c2v in ascending check order
+template <int D>
+__device__ __forceinline__ float ira_vn_info(const int32_t* __restrict__ row, int pos, int64_t so,
+                                             const float2* __restrict__ S, const uint32_t* __restrict__ MT, float app) {
+    float c[D];
+    int wrapped = 0;
+    static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
+        constexpr int t = decltype(TT)::value;
+        const int e = row[t];  // wave-uniform: a scalar load
+        const int ra = e & 0xff, sh = (e >> 8) & 0x1ff, slot = e >> 17;
+        int b = pos + sh;
+        const bool w = b >= kIZ;
+        b -= w ? kIZ : 0;
+        wrapped += w;
+        const int64_t i = so + (int64_t)ra * kIZ + b;
+        c[t] = ira_c2v(S[i], MT[i], slot);
+    });
+    // entries are sorted by x = a + q s, i.e. by s: the wrapped ones are the last `wrapped` entries and their
+    // checks come first in ascending order
+    const int rho = wrapped == 0 ? 0 : D - wrapped;
+    rotate_left<D>(c, rho);
+#pragma unroll
+    for (int t = 0; t < D; ++t) app = app + c[t];
+    return app;
+}
+
+// One task = one variable group (information group g < G, or parity row a = g - G) of one codeword; lanes =
+// the 360 positions.  Writes app in the permuted layout (information: g*360 + m, parity: k + a*360 + b).
+template <int MAXDV>
+__global__ __launch_bounds__(384) void k_ira_vn(IRADev t, const float* __restrict__ L, float* __restrict__ app,
+                                                const float2* __restrict__ S, const uint32_t* __restrict__ MT, int Bc) {
+    int cw, gi;
+    if (!ira_task(t.G + t.q, Bc, cw, gi)) return;
+    const int pos = threadIdx.x;
+    if (pos >= kIZ) return;
+    const int64_t vo = (int64_t)cw * t.n + (int64_t)gi * kIZ + pos;
+    const int64_t so = (int64_t)cw * t.M;
+    float a = L[vo];
+    if (gi < t.G) {
+        const int d = t.vdeg[gi];
+        const int32_t* row = t.vn + gi * kIVS;
+        static_for<1, MAXDV + 1>([&](auto DD) __attribute__((always_inline)) {
+            constexpr int D = decltype(DD)::value;
+            if (d == D) a = ira_vn_info<D>(row, pos, so, S, MT, a);
+        });
+    } else {
+        // parity p_j, j = r + q pos: checks j (its own (r, pos), slot kIPS) and j + 1 (slot kIPS + 1 there)
+        const int r = gi - t.G;
+        const int64_t i0 = so + (int64_t)r * kIZ + pos;
+        a = a + ira_c2v(S[i0], MT[i0], kIPS);
+        int r1 = r + 1, p1 = pos;
+        if (r1 == t.q) {
+            r1 = 0;
+            p1 = pos + 1;
+        }
+        if (p1 < kIZ) {  // j + 1 < M
+            const int64_t i1 = so + (int64_t)r1 * kIZ + p1;
+            a = a + ira_c2v(S[i1], MT[i1], kIPS + 1);
+        }
+    }
+    app[vo] = a;
+}
+
+// One task = one check row a of one codeword; lanes = positions b.  Reads the posteriors of the row's
+// variables and its own state, writes the new state (the oracle's k_cn_ms arithmetic on v2c = app - c2v).
+template <int MAXR>
+__global__ __launch_bounds__(384) void k_ira_cn(IRADev t, const float* __restrict__ app, float2* __restrict__ S,
+                                                uint32_t* __restrict__ MT, int Bc, float clamp, float alpha, float beta) {
+    int cw, ra;
+    if (!ira_task(t.q, Bc, cw, ra)) return;
+    const int pos = threadIdx.x;
+    if (pos >= kIZ) return;
+    const int64_t ao = (int64_t)cw * t.n;
+    const int64_t si = (int64_t)cw * t.M + (int64_t)ra * kIZ + pos;
+    const float2 st = S[si];
+    const uint32_t mt = MT[si];
+    const int R = t.cdeg[ra];
+    const int32_t* row = t.cn + ra * kICS;
+    float v[MAXR];
+    static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
+        constexpr int s = decltype(SS)::value;
+        if (s < R) {
+            const int e = row[s];
+            const int g = e & 0xff, sh = e >> 8;
+            int m = pos - sh;
+            m += m < 0 ? kIZ : 0;
+            v[s] = app[ao + (int64_t)g * kIZ + m] - ira_c2v(st, mt, s);
+        }
+    });
+    const float vp0 = app[ao + t.k + (int64_t)ra * kIZ + pos] - ira_c2v(st, mt, kIPS);
+    const bool has_prev = ra > 0 || pos > 0;  // check 0 has no p_{-1}
+    const int64_t pi = ra > 0 ? ao + t.k + (int64_t)(ra - 1) * kIZ + pos
+                              : ao + t.k + (int64_t)(t.q - 1) * kIZ + (pos > 0 ? pos - 1 : 0);
+    const float vp1 = app[pi] - ira_c2v(st, mt, kIPS + 1);
+    float min1 = __builtin_inff(), min2 = __builtin_inff();
+    int idx = -1;
+    uint32_t sgn = 0;
+    auto take = [&](float x, int s) __attribute__((always_inline)) {
+        const float m = fabsf(x);
+        sgn ^= f2u(x);
+        if (m < min1) {
+            min2 = min1;
+            min1 = m;
+            idx = s;
+        } else if (m < min2) {
+            min2 = m;
+        }
+    };
+    static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
+        constexpr int s = decltype(SS)::value;
+        if (s < R) take(v[s], s);
+    });
+    take(vp0, kIPS);
+    if (has_prev) take(vp1, kIPS + 1);
+    const float mag1 = ms_mag(min1, alpha, beta, clamp);
+    const float mag2 = ms_mag(min2, alpha, beta, clamp);
+    uint32_t meta = (uint32_t)idx << 27;
+    static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
+        constexpr int s = decltype(SS)::value;
+        if (s < R) meta |= ((sgn ^ f2u(v[s])) >> 31) << s;
+    });
+    meta |= ((sgn ^ f2u(vp0)) >> 31) << kIPS;
+    if (has_prev) meta |= ((sgn ^ f2u(vp1)) >> 31) << (kIPS + 1);
+    S[si] = make_float2(mag1, mag2);
+    MT[si] = meta;
+}
+
+// natural [B][n] llr -> permuted L = -llr: information part as is, parity block [360][q] (index b*q + a)
+// transposed to [q][360] through an LDS tile.  grid: x = tiles of one codeword, y = codeword.
+__global__ __launch_bounds__(256) void k_ira_load(const float* __restrict__ llr, float* __restrict__ L, int n, int k,
+                                                  int q) {
+    __shared__ float tile[64][65];
+    const int64_t base = (int64_t)blockIdx.y * n;
+    const int ninfo = (k + 1023) / 1024;
+    if ((int)blockIdx.x < ninfo) {
+        const int v0 = blockIdx.x * 1024;
+        for (int v = v0 + threadIdx.x; v < v0 + 1024 && v < k; v += 256) L[base + v] = -llr[base + v];
+        return;
+    }
+    const int tix = blockIdx.x - ninfo;
+    const int ta = (q + 63) / 64;
+    const int b0 = (tix / ta) * 64, a0 = (tix % ta) * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {  // rows b, columns a: coalesced along a in the natural layout
+        const int b = b0 + r, a = a0 + tx;
+        if (b < kIZ && a < q) tile[r][tx] = -llr[base + k + (int64_t)b * q + a];
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {  // rows a, columns b: coalesced along b in the permuted layout
+        const int a = a0 + r, b = b0 + tx;
+        if (b < kIZ && a < q) L[base + k + (int64_t)a * kIZ + b] = tile[tx][r];
+    }
+}
+
+// z = 0.5 app (the oracle's final layer for min-sum, bp.py:51's decision rule) back to the natural layout:
+// bits (np.round(p1) rule) and soft (p1 = 1 - sigmoid(z), or z).
+__global__ __launch_bounds__(256) void k_ira_out(const float* __restrict__ app, uint8_t* __restrict__ bits,
+                                                 float* __restrict__ soft, int soft_z, int n, int k, int q) {
+    __shared__ float tile[64][65];
+    const int64_t base = (int64_t)blockIdx.y * n;
+    const int ninfo = (k + 1023) / 1024;
+    auto put = [&](int64_t i, float z) __attribute__((always_inline)) {
+        if (bits) bits[i] = (uint8_t)Num<float>::bit(z);
+        if (soft) soft[i] = soft_z ? z : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-z));
+    };
+    if ((int)blockIdx.x < ninfo) {
+        const int v0 = blockIdx.x * 1024;
+        for (int v = v0 + threadIdx.x; v < v0 + 1024 && v < k; v += 256) put(base + v, 0.5f * app[base + v]);
+        return;
+    }
+    const int tix = blockIdx.x - ninfo;
+    const int ta = (q + 63) / 64;
+    const int b0 = (tix / ta) * 64, a0 = (tix % ta) * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int a = a0 + r, b = b0 + tx;
+        if (b < kIZ && a < q) tile[r][tx] = 0.5f * app[base + k + (int64_t)a * kIZ + b];
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int b = b0 + r, a = a0 + tx;
+        if (b < kIZ && a < q) put(base + k + (int64_t)b * q + a, tile[tx][r]);
+    }
+}
+
+// ---- host ------------------------------------------------------------------------------------------------
+
+IRASpec* ira_detect(int m, int n, const int32_t* rp, const int32_t* ci, int device) {
+    if (m <= 0 || n <= m || m % kIZ || (n - m) % kIZ) return nullptr;
+    const int M = m, k = n - m, q = m / kIZ, G = k / kIZ;
+    if (q > 255 || G > 255) return nullptr;
+    // parity part: row c holds k + c and (c >= 1) k + c - 1, nothing else above k
+    std::vector<int32_t> vdeg_all(k, 0);
+    for (int c = 0; c < M; ++c) {
+        int np = 0;
+        bool own = false, prev = false;
+        for (int e = rp[c]; e < rp[c + 1]; ++e) {
+            const int v = ci[e];
+            if (v >= k) {
+                ++np;
+                own |= v == k + c;
+                prev |= c > 0 && v == k + c - 1;
+            } else {
+                ++vdeg_all[v];
+            }
+        }
+        if (!own || np != (c > 0 ? 2 : 1) || (c > 0 && !prev)) return nullptr;
+    }
+    // information columns: column lists (ascending checks)
+    std::vector<int32_t> cptr(k + 1, 0), cchk;
+    for (int v = 0; v < k; ++v) cptr[v + 1] = cptr[v] + vdeg_all[v];
+    cchk.resize(cptr[k]);
+    {
+        std::vector<int32_t> fill(cptr.begin(), cptr.end() - 1);
+        for (int c = 0; c < M; ++c)
+            for (int e = rp[c]; e < rp[c + 1]; ++e)
+                if (ci[e] < k) cchk[fill[ci[e]]++] = c;
+    }
+    IRASpec* s = new IRASpec();
+    s->q = q; s->G = G; s->k = k; s->n = n; s->M = M; s->E = rp[M]; s->device = device;
+    std::vector<int32_t> vn((size_t)G * kIVS, 0), vdeg(G, 0), cn((size_t)q * kICS, 0), cdeg(q, 0);
+    std::vector<std::vector<std::pair<int, int>>> rows(q);  // (group, shift) per check row
+    bool ok = true;
+    for (int g = 0; g < G && ok; ++g) {
+        const int v0 = g * kIZ;
+        const int d = cptr[v0 + 1] - cptr[v0];
+        if (d < 1 || d > kIVS) { ok = false; break; }
+        std::vector<int> xs(cchk.begin() + cptr[v0], cchk.begin() + cptr[v0 + 1]);  // ascending = the x order
+        std::vector<int> want(d);
+        for (int mm = 1; mm < kIZ && ok; ++mm) {
+            const int v = v0 + mm;
+            if (cptr[v + 1] - cptr[v] != d) { ok = false; break; }
+            for (int t = 0; t < d; ++t) want[t] = (int)(((int64_t)xs[t] + (int64_t)mm * q) % M);
+            std::sort(want.begin(), want.end());
+            for (int t = 0; t < d; ++t)
+                if (cchk[cptr[v] + t] != want[t]) { ok = false; break; }
+        }
+        vdeg[g] = d;
+        s->maxdv = std::max(s->maxdv, d);
+        for (int t = 0; t < d && ok; ++t) {
+            const int a = xs[t] % q, sh = xs[t] / q;
+            const int slot = (int)rows[a].size();
+            if (slot >= kICS) { ok = false; break; }
+            rows[a].push_back({g, sh});
+            vn[(size_t)g * kIVS + t] = a | (sh << 8) | (slot << 17);
+        }
+    }
+    for (int a = 0; a < q && ok; ++a) {
+        cdeg[a] = (int)rows[a].size();
+        s->maxr = std::max(s->maxr, cdeg[a]);
+        for (int i = 0; i < cdeg[a]; ++i) cn[(size_t)a * kICS + i] = rows[a][i].first | (rows[a][i].second << 8);
+    }
+    if (!ok) {
+        delete s;
+        return nullptr;
+    }
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != device) (void)hipSetDevice(device);
+    auto up = [](int32_t** d, const std::vector<int32_t>& h) -> bool {
+        if (hipMalloc((void**)d, h.size() * 4) != hipSuccess) return false;
+        return hipMemcpy(*d, h.data(), h.size() * 4, hipMemcpyHostToDevice) == hipSuccess;
+    };
+    ok = up(&s->vn, vn) && up(&s->vdeg, vdeg) && up(&s->cn, cn) && up(&s->cdeg, cdeg);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    if (!ok) {
+        ira_free(s);
+        return nullptr;
+    }
+    return s;
+}
+
+void ira_free(IRASpec* s) {
+    if (!s) return;
+    (void)hipFree(s->vn);
+    (void)hipFree(s->vdeg);
+    (void)hipFree(s->cn);
+    (void)hipFree(s->cdeg);
+    delete s;
+}
+
+bool ira_supports(const IRASpec* s, const ldpc_params& p) {
+    if (!s) return false;
+    if (p.algo != LDPC_ALGO_MIN_SUM) return false;
+    if (p.flags & (LDPC_F_EARLY_STOP | LDPC_F_F64)) return false;
+    if (getenv("LDPC_NO_IRA")) return false;  // A/B against the generic kernels in one process
+    return s->maxdv <= 16 && s->maxr <= kICS;
+}
+
+// codewords per chunk: each chunk's arrays (8n + 12M bytes per codeword) stay in the 256 MiB Infinity Cache for
+// all its iterations; LDPC_IRA_BUDGET_MB overrides (0 = the whole batch in one pass)
+static int64_t ira_chunk(const IRASpec* s, int64_t B) {
+    const char* env = getenv("LDPC_IRA_BUDGET_MB");
+    const int64_t budget = (env ? (int64_t)atol(env) : 200) << 20;
+    if (budget <= 0) return B;
+    const int64_t per = 8 * (int64_t)s->n + 12 * (int64_t)s->M;
+    int64_t bc = budget / per / 8 * 8;
+    if (bc < 8) bc = 8;
+    return bc < B ? bc : B;
+}
+
+size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {
+    const int64_t bc = ira_chunk(s, B);
+    auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    return 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8) + a256((size_t)bc * s->M * 4);
+}
+
+int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params& p, uint8_t* bits, float* soft,
+               int32_t* iters_used, char* ws, hipStream_t st) {
+    const int64_t bc = ira_chunk(s, B);
+    auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    float* L = (float*)ws;
+    float* app = (float*)(ws + a256((size_t)bc * s->n * 4));
+    float2* S = (float2*)(ws + 2 * a256((size_t)bc * s->n * 4));
+    uint32_t* MT = (uint32_t*)(ws + 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8));
+    const IRADev t{s->vn, s->vdeg, s->cn, s->cdeg, s->q, s->G, s->k, s->n, s->M};
+    const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
+    const unsigned tiles = (unsigned)((s->k + 1023) / 1024 + ((kIZ + 63) / 64) * ((s->q + 63) / 64));
+    for (int64_t o = 0; o < B; o += bc) {
+        const int b = (int)(B - o < bc ? B - o : bc);
+        const int64_t vo = o * s->n;
+        const unsigned cw8 = (unsigned)((b + 7) / 8) * 8;
+        k_ira_load<<<dim3(tiles, b), 256, 0, st>>>(llr + vo, L, s->n, s->k, s->q);
+        if (hipMemsetAsync(S, 0, (size_t)b * s->M * 8, st) != hipSuccess ||
+            hipMemsetAsync(MT, 0, (size_t)b * s->M * 4, st) != hipSuccess)
+            return set_error(LDPC_EHIP, "IRA state init failed");
+        const unsigned gvn = cw8 * (unsigned)(s->G + s->q), gcn = cw8 * (unsigned)s->q;
+        for (int it = 0; it <= p.iters; ++it) {
+            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, 384, 0, st>>>(t, L, app, S, MT, b);
+            else k_ira_vn<16><<<gvn, 384, 0, st>>>(t, L, app, S, MT, b);
+            if (it == p.iters) break;  // the last VN pass is the final layer's posterior
+            if (s->maxr <= 8) k_ira_cn<8><<<gcn, 384, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta);
+            else k_ira_cn<kICS><<<gcn, 384, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta);
+        }
+        k_ira_out<<<dim3(tiles, b), 256, 0, st>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
+                                                  s->n, s->k, s->q);
+    }
+    if (iters_used) fill_i32(iters_used, B, p.iters, st);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(LDPC_EHIP, "IRA kernel launch: %s", hipGetErrorString(e));
+    return LDPC_OK;
+}
+
+}  // namespace ldpc

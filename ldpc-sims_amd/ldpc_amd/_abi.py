@@ -22,7 +22,7 @@ EXPORTS = (
     "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
     "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_adc_quantize", "ldpc_weights_layout",
     "ldpc_decode_weighted", "ldpc_decode_x0", "ldpc_decode_bits_host", "ldpc_last_error", "ldpc_device_count",
-    "ldpc_version",
+    "ldpc_version", "ldpc_kernel_path",
 )
 
 
@@ -94,6 +94,8 @@ def load(path: str | None = None):
         getattr(L, f).restype = ctypes.c_int
     L.ldpc_last_error.restype = ctypes.c_char_p
     L.ldpc_version.restype = ctypes.c_char_p
+    L.ldpc_kernel_path.argtypes = [vp, ctypes.POINTER(Params)]
+    L.ldpc_kernel_path.restype = ctypes.c_char_p
     L._ldpc_path = p
     if path is None:
         _lib = L

@@ -81,6 +81,13 @@ class Decoder:
         return Params(int(iters), _ALGOS[algo], flags, float(clamp), float(alpha), float(beta), int(qmax),
                       int(app_max), float(qstep))
 
+    def kernel_path(self, p: Params) -> str:
+        """The kernel family a decode with these params runs: "qc-z<Z>", "ira-z360" or "generic-csr"."""
+        s = self.lib.ldpc_kernel_path(self._h, ctypes.byref(p))
+        if s is None:
+            raise _abi.LdpcError(_abi.LDPC_EINVAL, self.lib.ldpc_last_error().decode(errors="replace"))
+        return s.decode()
+
     def workspace_bytes(self, B: int, p: Params) -> int:
         out = ctypes.c_size_t()
         check(self.lib.ldpc_workspace_size(self._h, int(B), ctypes.byref(p), ctypes.byref(out)))

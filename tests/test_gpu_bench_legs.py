@@ -84,7 +84,7 @@ def test_config3_leg_full_batch_vs_oracle():
 
 def test_config4_leg_full_batch_vs_oracle():
     la, wl = _workload("config4")
-    assert wl.B == 4096 and la.iters == 50 and wl.kpath == "generic-csr"
+    assert wl.B == 4096 and la.iters == 50 and wl.kpath == "ira-z360"
     i = 3                                                    # Eb/N0 1.5 dB: the waterfall
     bench_bits = _counts_match(wl, i)
     x = wl.llrs[i]

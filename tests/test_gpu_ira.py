@@ -1,0 +1,138 @@
+"""GPU parity of the DVB-S2-structured min-sum kernels (csrc/ira.hip; BASELINE config [4]): bits AND soft z bit
+for bit against the C oracle (oracle/ldpc_oracle.c ms_f32, the flooding min-sum the generic kernels also match)
+and against the generic CSR kernels on the same batch, at config [4]'s 50 iterations and at the edges: 0 and
+1 iterations, exact-zero and negative-zero LLRs (the sign rules of v2c = app - c2v), saturating LLRs, a
+batch that is not a multiple of the 8-codeword XCD group, several Infinity-Cache chunk sizes, normalised and
+offset min-sum, and the DVB-S2-shaped code with other table addresses.  The reference cannot instantiate a
+code of this size (dense E x E masks, masking.py:36-38): parity here is against the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import ldpc_amd  # noqa: E402
+from ldpc_amd.codes import IRAEncoder, get_code  # noqa: E402
+
+
+def _llr(code, B, ebn0, seed):
+    rng = np.random.default_rng(seed)
+    enc = IRAEncoder(code)
+    cw = enc.encode(rng.integers(0, 2, size=(B, enc.k)))
+    sigma = np.sqrt(1.0 / (2 * 0.5 * 10 ** (ebn0 / 10)))
+    return cw, (-2.0 * ((1.0 - 2.0 * cw) + sigma * rng.standard_normal(cw.shape)) / sigma**2).astype(np.float32)
+
+
+def _decode(dec, x, iters, **kw):
+    r = dec.decode(torch.from_numpy(x).cuda(), iters, algo="minsum", soft="z", want_iters=True, **kw)
+    torch.cuda.synchronize()
+    return r["bits"].cpu().numpy(), r["soft"].cpu().numpy(), r["iters_used"].cpu().numpy()
+
+
+def _same(a, b):
+    return np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.fixture(scope="module")
+def dvbs2():
+    H, _ = get_code("dvbs2_12")
+    return H, ldpc_amd.get_decoder(H)
+
+
+def test_kernel_path_selection(dvbs2):
+    H, dec = dvbs2
+    assert dec.kernel_path(dec.params(50, "minsum", 20.0)) == "ira-z360"
+    assert dec.kernel_path(dec.params(50, "minsum", 20.0, alpha=0.75, beta=0.5)) == "ira-z360"
+    # not (yet) covered by the IRA kernels: the generic CSR kernels take them
+    assert dec.kernel_path(dec.params(50, "minsum", 20.0, force_generic=True)) == "generic-csr"
+    assert dec.kernel_path(dec.params(50, "minsum", 20.0, early_stop=True)) == "generic-csr"
+    assert dec.kernel_path(dec.params(50, "tanh", 20.0)) == "generic-csr"
+    wifi = ldpc_amd.get_decoder(get_code("wifi648_12")[0])
+    assert wifi.kernel_path(wifi.params(50, "minsum", 20.0)) == "qc-z27"
+    peg = ldpc_amd.get_decoder(get_code("peg64_32")[0])
+    assert peg.kernel_path(peg.params(5, "minsum", 20.0)) == "generic-csr"
+
+
+@pytest.mark.parametrize("ebn0", [0.8, 1.2, 1.6])
+def test_config4_50it_vs_oracle_bitwise(dvbs2, ebn0):
+    """Config [4] itself (50 iterations, clamp 20, plain min-sum) around the waterfall: bits and z bitwise."""
+    H, dec = dvbs2
+    _, x = _llr(H, 21, ebn0, seed=int(ebn0 * 10))          # 21: not a multiple of the 8-codeword XCD group
+    bits, z, used = _decode(dec, x, 50, clamp=20.0)
+    ref = oracle.ms_f32(H, x, 50, 20.0)
+    assert np.array_equal(bits, ref["bits"])
+    assert _same(z, ref["z"])
+    assert (used == 50).all()
+
+
+@pytest.mark.parametrize("alpha,beta,clamp", [(0.75, 0.0, 20.0), (1.0, 0.5, 20.0), (0.8125, 0.25, 6.0)])
+def test_normalised_offset_vs_oracle(dvbs2, alpha, beta, clamp):
+    H, dec = dvbs2
+    _, x = _llr(H, 9, 1.0, seed=3)
+    bits, z, _ = _decode(dec, x, 20, clamp=clamp, alpha=alpha, beta=beta)
+    ref = oracle.ms_f32(H, x, 20, clamp, alpha, beta)
+    assert np.array_equal(bits, ref["bits"]) and _same(z, ref["z"])
+
+
+@pytest.mark.parametrize("iters", [0, 1, 2, 7])
+def test_few_iterations_and_signed_zeros(dvbs2, iters):
+    """Exact zeros of both signs and saturating values among the LLRs: the first VN pass must form L + 0
+    (a -0 LLR gives +0, as the oracle's app += 0), and v2c = app - c2v keeps the oracle's sign bits."""
+    H, dec = dvbs2
+    _, x = _llr(H, 10, 1.4, seed=11 + iters)
+    rng = np.random.default_rng(iters)
+    mask = rng.random(x.shape)
+    x[mask < 0.02] = 0.0
+    x[(mask >= 0.02) & (mask < 0.04)] = -0.0
+    x[(mask >= 0.04) & (mask < 0.045)] = 1e30
+    x[(mask >= 0.045) & (mask < 0.05)] = -1e30
+    bits, z, _ = _decode(dec, x, iters, clamp=20.0)
+    ref = oracle.ms_f32(H, x, iters, 20.0)
+    assert np.array_equal(bits, ref["bits"]) and _same(z, ref["z"])
+
+
+def test_equals_generic_kernels_and_chunking(dvbs2, monkeypatch):
+    """The IRA path equals the generic CSR kernels bit for bit on one batch, whatever the Infinity-Cache chunk
+    (one pass, 8-codeword chunks with a ragged last chunk, the default)."""
+    H, dec = dvbs2
+    _, x = _llr(H, 45, 1.3, seed=5)
+    gb, gz, _ = _decode(dec, x, 12, clamp=20.0, force_generic=True)
+    for budget in ("0", "1", None):
+        if budget is None:
+            monkeypatch.delenv("LDPC_IRA_BUDGET_MB", raising=False)
+        else:
+            monkeypatch.setenv("LDPC_IRA_BUDGET_MB", budget)
+        bits, z, _ = _decode(dec, x, 12, clamp=20.0)
+        assert np.array_equal(bits, gb) and _same(z, gz), budget
+
+
+def test_shaped_code_and_host_pointers():
+    """The DVB-S2-shaped code (other table addresses, same degree profile) through host pointers, soft p1."""
+    H, _ = get_code("dvbs2s_12")
+    dec = ldpc_amd.get_decoder(H)
+    assert dec.kernel_path(dec.params(30, "minsum", 20.0)) == "ira-z360"
+    _, x = _llr(H, 6, 1.2, seed=9)
+    r = dec.decode(x, 30, algo="minsum", clamp=20.0, soft="p1")
+    g = dec.decode(x, 30, algo="minsum", clamp=20.0, soft="p1", force_generic=True)
+    ref = oracle.ms_f32(H, x, 30, 20.0)
+    assert np.array_equal(r["bits"], ref["bits"]) and np.array_equal(r["bits"], g["bits"])
+    assert _same(r["soft"], g["soft"])
+
+
+def test_not_ira_when_structure_breaks():
+    """A DVB-S2 H with one information edge moved is no longer IRA-structured: the generic kernels take it."""
+    H, _ = get_code("dvbs2_12")
+    from ldpc_amd.codes import SparseCode
+    rp, ci = H.row_ptr.copy(), H.col_idx.copy()
+    e = rp[100] + 1                        # an information edge of check 100: move it to a column it lacks
+    row = set(ci[rp[100]:rp[101]].tolist())
+    new = next(c for c in range(ci[e] + 1, H.k) if c not in row)
+    ci[e] = new
+    ci[rp[100]:rp[101]].sort()
+    broken = SparseCode(H.m, H.n, rp, ci, name="broken")
+    dec = ldpc_amd.get_decoder(broken)
+    assert dec.kernel_path(dec.params(10, "minsum", 20.0)) == "generic-csr"

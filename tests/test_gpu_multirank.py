@@ -123,7 +123,7 @@ def test_bench_dvbs2_config4_two_ranks_equal_one_process():
     two = _bench_line(_launch([*common, "--gpus", "2", "--batch", "256"], 2, timeout=400))
     one = _bench_line(_launch([*common, "--gpus", "1", "--batch", "512"], 1, timeout=400))
     assert two["ranks"]["world_size"] == 2 and two["config"]["global_batch"] == 512
-    assert two["config"]["kernel_path"] == "generic-csr" and two["config"]["iters"] == 50
+    assert two["config"]["kernel_path"] == "ira-z360" and two["config"]["iters"] == 50
     assert two["ber"]["codewords_per_point"] == one["ber"]["codewords_per_point"] == 512
     assert two["ber"]["coded_ber_info"] == one["ber"]["coded_ber_info"]
     assert two["ber"]["coded_bler"] == one["ber"]["coded_bler"]
@@ -144,7 +144,7 @@ def test_bench_multigpu_runs_the_config4_leg():
     assert list(two["side"]["configs"]) == ["config4"] and list(one["side"]["configs"]) == ["config4"]
     assert l2["n_gpus"] == 2 and l2["config"]["code"] == "dvbs2_12" and l2["config"]["iters"] == 50
     assert l2["config"]["batch_per_gpu"] == 256 and l2["config"]["global_batch"] == 512
-    assert l2["config"]["kernel_path"] == "generic-csr"
+    assert l2["config"]["kernel_path"] == "ira-z360"
     rk = l2["ranks"]
     assert rk["world_size"] == 2 and [r["rank"] for r in rk["per_rank"]] == [0, 1]
     assert all(r["timed_s"] > 0 for r in rk["per_rank"])

@@ -113,7 +113,7 @@ __device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
 // (D, S) ~ (P+ - P-, P+ + P-) with P+- = prod(1 +- a); the identity is (0, 1), one edge adds D' = D + a*S,
 // S' = S + a*D (two fma), two sets join as D = Dp*Sq + Sp*Dq, S = Sp*Sq + Dp*Dq (one product and one fma
 // each, ds_join_out; an edge with s = +-0, a = 1, keeps D == S exactly through pushes and as a join's suffix,
-// to an ulp as its prefix).  The check output of an edge is
+// to an ulp as its prefix — so such edges are handled explicitly, ds_fix_one).  The check output of an edge is
 // log(S/D) of the set of the others (= log((1+|p|)/(1-|p|))), at most log RMAX where RMAX =
 // (1+pmax)/(1-pmax) = 16777215 is the reference's fp32 p clamp (bp_cv.py:44-47) exactly, and at most the
 // caller's clamp (bp.py:47); its sign the xor of the others' signs.
@@ -141,8 +141,18 @@ __device__ __forceinline__ float sp_vn_arg(float L, float sum2) { return __built
 
 // signed a = copysign(exp(-|s|), s) of a VC sum s2 = s * log2 e: one v_exp_f32 of -|s2|.  A relative error of
 // ulp(s2) in s2 moves the check output log(S/D) by at most that much absolutely; |s| beyond the clamp saturates.
+// DS_CR (diagnostic builds only, scripts/trace_config2.py): bit 0 / 1 / 2 evaluate exp2 / the division S/D / log2
+// correctly rounded (through fp64, the oracle's exp2f / S / D / log2f) instead of v_exp_f32 / S * v_rcp_f32(D) /
+// v_log_f32, to name the operation that separates the kernels from their specification.  Shipped: 0.
+#ifndef DS_CR
+#define DS_CR 0
+#endif
 __device__ __forceinline__ float vn_signed_a(float x2) {
+#if DS_CR & 1
+    return __builtin_copysignf((float)exp2(-(double)fabsf(x2)), x2);
+#else
     return __builtin_copysignf(__builtin_amdgcn_exp2f(-fabsf(x2)), x2);
+#endif
 }
 
 // SP_TIE(operands): the serial-chain tie of the tanh-SP kernels, an empty asm that redefines the chain's
@@ -201,8 +211,16 @@ __device__ __forceinline__ DSet ds_push(DSet x, float a) {  // a = |signed a| of
 // log2(S/D) of a set clamped to [0, cmax2] (S >= D; a rounding below 1 gives 0; D == 0: +inf -> cmax2), with
 // the given sign bit (bit 31 of sgn)
 __device__ __forceinline__ float ds_out(float D, float S, uint32_t sgn, float cmax2) {
+#if DS_CR & 2
+    const float r = (float)((double)S / (double)D);  // S, D exact in fp64: one rounding = the oracle's S / D
+#else
     const float r = S * __builtin_amdgcn_rcpf(D);
+#endif
+#if DS_CR & 4
+    const float y = __builtin_amdgcn_fmed3f((float)log2((double)r), 0.0f, cmax2);
+#else
     const float y = __builtin_amdgcn_fmed3f(__builtin_amdgcn_logf(r), 0.0f, cmax2);
+#endif
     return u2f(f2u(y) | (sgn & 0x80000000u));
 }
 // the output of an edge from its prefix set p and suffix set q (the join, then ds_out).  DS_JOIN_FMA: each of
@@ -246,7 +264,36 @@ __device__ __forceinline__ void ds_tie(DSet& pre, float (&g)[d]) {
     if constexpr (LAG == 0) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t]));
     else if constexpr (t >= LAG) SP_TIE("+v"(pre.D), "+v"(pre.S), "+v"(g[t - LAG]));
 }
-template <int d, int SERIAL, int LAG = 0, int BLOCK = DS_BLOCK>
+// Edges with a == 1 (s = +-0: the reference's tanh(0) = 0 makes p exactly 0 for every OTHER edge of the check,
+// bp_cv.py:38-50): an edge whose exclusive set holds one outputs exactly +-0 (oracle cn_stable_f32).  The (D, S)
+// sets give that by themselves except through a join with such a PREFIX (an ulp apart, DS_JOIN_FMA) and S/D
+// rounded through v_rcp_f32, and several such edges per check (erasures, quantized LLRs) add up to a flipped
+// hard decision (tests/golden/bp_zeros.npz).  cn_ds_row<..., FIX = true> marks the row's a == 1 edges in the low
+// bits of the row's sign word (whose bit 31 alone the outputs read, so no register is added) and resets each
+// output whose other edges include one to its sign bit as it is formed.  The register kernels run their whole
+// iteration loop in that form for a wave (or unit) whose LLRs hold an exact zero — the source of a == 1 edges:
+// s = 0 needs L = 0 or an exact cancellation — and in the plain form otherwise, so the common path keeps its
+// registers and schedule; the generic kernels apply the rule always.
+#ifndef QC_SP_FIXZ
+#define QC_SP_FIXZ 1  // register kernels: the FIX loop for waves / units with an exact-zero LLR (0: never)
+#endif
+template <int d>
+__device__ __forceinline__ uint32_t ds_ones(const float (&g)[d]) {
+    uint32_t ones = 0;
+    static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
+        constexpr int t = decltype(tt)::value;
+        ones |= (fabsf(g[t]) == 1.0f ? 1u : 0u) << t;
+    });
+    return ones;
+}
+// output y of edge t of a row whose a == 1 edges are marked in bits 0..30 of sgw: +-0 if another edge is marked
+template <int t>
+__device__ __forceinline__ float ds_fix_one(float y, uint32_t sgw) {
+    static_assert(t < 31, "the a == 1 marks share the sign word with its bit 31");
+    return (sgw & 0x7fffffffu & ~(1u << t)) ? u2f(f2u(y) & 0x80000000u) : y;
+}
+
+template <int d, int SERIAL, int LAG = 0, int BLOCK = DS_BLOCK, bool FIX = false>
 __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
     const float clamp = cmax2;  // (log2 units, sp_cmax2)
     constexpr auto tie_after = [](int t) { return SERIAL > 0 && (t + 1) % SERIAL == 0; };
@@ -258,6 +305,7 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
         sg = __builtin_amdgcn_bitop3_b32(sg, f2u(g[k]), f2u(g[k + 1]), 0x96);
     });
     if constexpr (d % 2 == 0) sg ^= f2u(g[d - 1]);
+    if constexpr (FIX && d > 1) sg = (sg & 0x80000000u) | ds_ones(g);  // the row's a == 1 edges (ds_fix_one)
     if constexpr (d == 1) {
         g[0] = ds_out(0.0f, 1.0f, 0u, clamp);  // empty product: p = 1 -> the ceiling, positive
     } else if constexpr (d > DS_SPLIT_D) {
@@ -327,6 +375,7 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
                 if constexpr (t == 0) y = ds_out(sD[1 - lo], sS[1 - lo], sg ^ f2u(g[t]), clamp);
                 else if constexpr (t == d - 1) y = ds_out(pre.D, pre.S, sg ^ f2u(g[t]), clamp);
                 else y = ds_join_out(pre, {sD[t + 1 - lo], sS[t + 1 - lo]}, sg ^ f2u(g[t]), clamp);
+                if constexpr (FIX) y = ds_fix_one<t>(y, sg);
                 if constexpr (t == 0) pre = {a, 1.0f};
                 else if constexpr (t < d - 1) pre = ds_push(pre, a);
                 g[t] = y;
@@ -345,16 +394,19 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
         });
         DSet pre = {fabsf(g[0]), 1.0f};
         g[0] = ds_out(sD[1], sS[1], sg ^ f2u(g[0]), clamp);
+        if constexpr (FIX) g[0] = ds_fix_one<0>(g[0], sg);
         if constexpr (tie_after(0)) SP_TIE("+v"(pre.D), "+v"(g[0]));
         static_for<1, d - 1>([&](auto tt) __attribute__((always_inline)) {
             constexpr int t = decltype(tt)::value;
             const float a = fabsf(g[t]);
-            const float y = ds_join_out(pre, {sD[t + 1], sS[t + 1]}, sg ^ f2u(g[t]), clamp);
+            float y = ds_join_out(pre, {sD[t + 1], sS[t + 1]}, sg ^ f2u(g[t]), clamp);
+            if constexpr (FIX) y = ds_fix_one<t>(y, sg);
             pre = ds_push(pre, a);
             g[t] = y;
             if constexpr (tie_after(t)) ds_tie<t, LAG>(pre, g);
         });
         g[d - 1] = ds_out(pre.D, pre.S, sg ^ f2u(g[d - 1]), clamp);
+        if constexpr (FIX) g[d - 1] = ds_fix_one<d - 1>(g[d - 1], sg);
     }
 }
 

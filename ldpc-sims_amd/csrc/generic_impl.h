@@ -399,8 +399,14 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
             }
         });
         DSet pre[V];
+        int n1[V];  // edges with a == 1: every other edge outputs exactly +-0 (common.h ds_fix_ones)
 #pragma unroll
-        for (int i = 0; i < V; ++i) pre[i] = ds_identity();
+        for (int i = 0; i < V; ++i) {
+            pre[i] = ds_identity();
+            n1[i] = 0;
+#pragma unroll
+            for (int k = 0; k < MAXD; ++k) n1[i] += (k < d && fabsf(t[k].x[i]) == 1.0f) ? 1 : 0;
+        }
         static_for<0, MAXD>([&](auto ee) __attribute__((always_inline)) {
             constexpr int e = decltype(ee)::value;
             if (e < d) {
@@ -408,6 +414,7 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
 #pragma unroll
                 for (int i = 0; i < V; ++i) {
                     o.x[i] = ds_join_out(pre[i], suf[e + 1][i], sg[i] ^ f2u(t[e].x[i]), cmax2);
+                    if (n1[i] - (fabsf(t[e].x[i]) == 1.0f ? 1 : 0) > 0) o.x[i] = u2f(f2u(o.x[i]) & 0x80000000u);
                     pre[i] = ds_push(pre[i], fabsf(t[e].x[i]));
                 }
                 store_live<T, V, ES>(c2v + (int64_t)(a + e) * ldb + cw, o, done + cw);

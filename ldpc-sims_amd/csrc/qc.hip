@@ -1146,7 +1146,10 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 // each check's frame on the scalar unit (as k_qc_ms_st); a codeword whose syndrome is zero stops with
 // iters_used = it and its z_it is parked in its own L region of LDS (its lanes keep computing for the
 // wave's other codeword, discarded).  Bitwise equal to the generic path's early stop.
-template <class C, bool EARLY>
+// PASS (the a == 1 rule, common.h cn_ds_row FIX): 1 = the plain loop for waves without an exact-zero LLR (the
+// others return at once), 2 = the FIX loop for the waves with one (the others return) — two launches, so each
+// kernel keeps its own register allocation; 0 = the plain loop for every wave (QC_SP_FIXZ 0).
+template <class C, bool EARLY, int PASS = 1>
 __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const float* __restrict__ llr, int64_t B, int iters,
                                                                        float clamp, int flags, uint8_t* __restrict__ bits,
                                                                        float* __restrict__ soft, int32_t* __restrict__ iters_used) {
@@ -1196,6 +1199,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     __shared__ float Ls[(sp_tpb<EARLY>() / 64) * CPW * N];
     const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
     const int lbase4 = lbase * 4;  // bytes (lds_reload)
+    bool zl = false;  // an exact-zero LLR in this lane's variables (common.h cn_ds_row FIX)
     {
         const int64_t cwbase = valid ? cw * N : 0;
         const float vmask = valid ? 1.0f : 0.0f;
@@ -1204,8 +1208,15 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
             int t = z + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const float x = llr[cwbase + j * Z + (valid ? t : 0)] * vmask;
+            zl |= valid && x == 0.0f;
             if (z < Z) Ls[lbase + j * Z] = -x;  // L = -llr (bp.py:47)
         });
+    }
+    // a wave whose codewords hold an exact-zero LLR runs the loop with the a == 1 rule (PASS 2); every other wave
+    // the plain loop (PASS 1; the rule changes nothing there unless an s cancels exactly)
+    if constexpr (PASS != 0) {
+        const bool zin = __ballot(zl) != 0;
+        if (zin != (PASS == 2)) return;
     }
     float msg[NE];
 #pragma unroll
@@ -1217,6 +1228,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
 
     // QC_SP_MASK_IDLE (fixed count): idle lanes (z >= Z) sit the iteration loop out, EXEC-masked (as QC_PH_MASK_IDLE)
     const bool loop_lane = !(QC_SP_MASK_IDLE && !EARLY) || z < Z;
+    constexpr bool FIX = PASS == 2;
     if (loop_lane)
     for (int it = 0; it < iters; ++it) {
         if constexpr (EARLY) {
@@ -1369,7 +1381,8 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
                 }
             });
             if constexpr (!EARLY && QC_SP_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-            cn_ds_row<d, (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32))) ? QC_SP_SERIAL_STRIDE : 0>(g, cmax2);
+            cn_ds_row<d, (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32))) ? QC_SP_SERIAL_STRIDE : 0, 0, DS_BLOCK,
+                      FIX>(g, cmax2);
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int s = C::SHR[r][t];
@@ -1446,7 +1459,12 @@ static int launch_sp_es(const void* llr, int64_t B, const ldpc_params& p, uint8_
     const int64_t waves = (B + CPW - 1) / CPW;
     const int tpb = sp_tpb<true>();
     const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
-    k_qc_sp_st<C, true><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used);
+    if constexpr (QC_SP_FIXZ) {
+        k_qc_sp_st<C, true, 1><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used);
+        k_qc_sp_st<C, true, 2><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used);
+    } else {
+        k_qc_sp_st<C, true, 0><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
     return LDPC_OK;
@@ -1507,9 +1525,16 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
                 else return qc_launch_ms_es_wifi1296_23(llr, B, p, bits, soft, used, st);
             }
         } else {
-            if (es) k_qc_sp_st<C, true><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+            if (es) k_qc_sp_st<C, true, 0><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
         }
-        if (!es) k_qc_sp_st<C, false><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+        if (!es) {
+            if constexpr (QC_SP_FIXZ) {  // the plain pass, then the a == 1 rule's pass for waves with a zero LLR
+                k_qc_sp_st<C, false, 1><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+                k_qc_sp_st<C, false, 2><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+            } else {
+                k_qc_sp_st<C, false, 0><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+            }
+        }
     } else if (p.algo == LDPC_ALGO_QMIN_SUM && QC_PACKED != 0) {
         // two codewords per lane in packed fp16 (qc_pk.hip)
         if constexpr (std::is_same_v<C, Wifi648_12>) return qc_launch_qms_pk_wifi648_12(llr, B, p, bits, soft, used, st);

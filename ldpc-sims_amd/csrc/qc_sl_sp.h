@@ -85,7 +85,9 @@ __device__ __forceinline__ void sl_barrier() {
     if constexpr (!QC_SL_DIAG_NOBAR) __syncthreads();
 }
 
-template <class C, bool EARLY>
+// PASS: as k_qc_sp_st's (qc.hip) — 1 = the plain loop for units without an exact-zero LLR, 2 = the a == 1 rule's
+// loop for units with one, 0 = the plain loop for every unit
+template <class C, bool EARLY, int PASS = 1>
 __global__ __launch_bounds__(C::S * 64)
 __attribute__((amdgpu_waves_per_eu(EARLY ? QC_SL_SP_WAVES_PER_SIMD_EARLY : QC_SL_SP_WAVES_PER_SIMD)))
 void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
@@ -113,6 +115,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     const float* const lp = llr + (valid ? cw * N : 0);
     const int lb = h * NB * Z + zc;
     float Lr[LM == 0 ? NB : 1];
+    bool zl = false;  // an exact-zero LLR among this lane's variables
     auto Lr_at = [&](int j) __attribute__((always_inline)) {
         if constexpr (LM == 2) {
             int z = zc;
@@ -134,14 +137,20 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
             int t = zc + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const float x = valid ? -lp[j * Z + t] : 0.0f;
+            zl |= valid && x == 0.0f;
             if constexpr (LM == 1) {
                 if (live) Lsh[lb + j * Z] = x;
             } else {
                 Lr[j] = x;
             }
         });
-        if constexpr (LM == 1) __syncthreads();
+    } else {
+        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) { zl |= valid && Lr_at(decltype(jj)::value) == 0.0f; });
     }
+    // the unit's two codewords hold an exact-zero LLR: the loop with the a == 1 rule (common.h cn_ds_row FIX);
+    // the barrier also orders the L rows of LM == 1
+    const bool zin = __syncthreads_or(zl);
+    if (PASS != 0 && zin != (PASS == 2)) return;  // uniform over the unit
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
@@ -174,6 +183,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     bool done0 = cwp >= B, done1 = cwp + 1 >= B;  // a missing codeword counts as converged
     int used0 = iters, used1 = iters;
 
+    constexpr bool FIX = PASS == 2;
     for (int it = 0; it < iters; ++it) {
         if constexpr (EARLY) {
             if (it > 0) {
@@ -270,7 +280,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
                 if constexpr (s == 0) g[t] = msg[e0 + t];
                 else g[t] = Xv[nz_index<C>(r, t) * ROW + xb + s];
             });
-            cn_ds_row<d, QC_SL_SP_SERIAL_ROW>(g, cmax2);  // O(d) exclusive sets (common.h)
+            cn_ds_row<d, QC_SL_SP_SERIAL_ROW, 0, DS_BLOCK, FIX>(g, cmax2);  // O(d) exclusive sets (common.h)
             if constexpr (CMP) sl_barrier();  // every wave has read this row's v2c before the buffer takes its c2v
             if (live) {
                 static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
@@ -402,7 +412,7 @@ constexpr int rs_q() {  // the smallest Q with Q * Q >= Z (9 for 81)
     return q;
 }
 
-template <class C>
+template <class C, int PASS = 1>  // PASS: as k_qc_sp_sl's
 __global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_RS_WAVES_PER_SIMD)))
 void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
                 uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
@@ -462,9 +472,16 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
         t -= (t >= Z) ? Z : 0;
         return lval ? -lp[j * Z + t] : 0.0f;
     };
+    bool zl = false;  // an exact-zero LLR among this lane's variables
     if constexpr (QC_RS_L == 0) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) Lreg[j] = Lload(j, false);
+        for (int j = 0; j < NB; ++j) {
+            Lreg[j] = Lload(j, false);
+            zl |= valid && Lreg[j] == 0.0f;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NB; ++j) zl |= valid && Lload(j, false) == 0.0f;
     }
     auto Lr_at = [&](int j) __attribute__((always_inline)) {
         if constexpr (QC_RS_L == 0) return Lreg[j];
@@ -480,7 +497,10 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
             });
         });
     }
-    __syncthreads();
+    // (every check slot zeroed) and: the unit's codewords hold an exact-zero LLR -> the loop with the a == 1
+    // rule (common.h cn_ds_row FIX)
+    const bool zin = __syncthreads_or(zl);
+    if (PASS != 0 && zin != (PASS == 2)) return;  // uniform over the unit
     const float cmax2 = sp_cmax2(clamp);  // check outputs in log2 units (common.h)
     // column j's messages in ascending row order: (row, slot) of its k-th edge
     auto col_rt = [](int j, int kk) constexpr {
@@ -510,6 +530,7 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
     // QC_RS_MASK_IDLE: idle lanes (l >= ZL) sit the iteration loop out, EXEC-masked (they never store; every wave
     // keeps live lanes, so each still meets both barriers of every iteration)
     const bool loop_lane = !QC_RS_MASK_IDLE || live;
+    constexpr bool FIX = PASS == 2;
     if (loop_lane)
     for (int it = 0; it < iters; ++it) {
         // VN phase (variable frame): every column's c2v -> v2c as signed a, written back in place
@@ -583,7 +604,7 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
             });
             if constexpr (QC_RS_PRIO == 3) __builtin_amdgcn_s_setprio(0);
             if constexpr (QC_RS_CPF > 0 && r + 1 < MB) cpf(std::integral_constant<int, r + 1>{});
-            cn_ds_row<d, QC_RS_SERIAL_ROW, QC_RS_ROW_LAG, QC_RS_DS_BLOCK>(g, cmax2);  // O(d) exclusive sets (common.h)
+            cn_ds_row<d, QC_RS_SERIAL_ROW, QC_RS_ROW_LAG, QC_RS_DS_BLOCK, FIX>(g, cmax2);  // O(d) exclusive sets (common.h)
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 if constexpr (C::SHR[r][t] == 0) m0[rs_zero_index<C>(r, t)] = g[t];

@@ -81,8 +81,11 @@ static int syndrome_ok(const graph_t* g, const uint8_t* bits);
  * (1-p cancels; one ulp of tanh near 1 is a 1e-4..1e-3 error in log).  Exclusive (D, S) per edge from prefix
  * and suffix sets, O(d) per check.  The clamp |p| <= 1-1e-7 is S/D <= RMAX = (1+pmax)/(1-pmax) (fp32:
  * 16777215 = the reference's fp32 bound exactly), then the caller's clamp; sign = xor of the others' signs.
- * An s of +-0 gives a = 1, whose set has D == S exactly (pushes and a join with such a suffix keep it so;
- * a join with such a prefix to within an ulp): log 1 = 0 for the other edges, as the reference's p = 0.
+ * An s of +-0 gives a = 1 — the reference's tanh(0) = 0 makes p exactly 0 for every OTHER edge of the check,
+ * whose output is then log 1 = 0: an edge whose exclusive set holds an a == 1 edge outputs exactly 0 (its sign
+ * bit as any other output's).  (Pushes and a join with such a suffix keep D == S exactly, but the fma join with
+ * such a prefix only to an ulp, which several zeros per check — erasures, quantized LLRs — add up to a flipped
+ * hard decision: tests/golden/bp_zeros.npz.)
  * Messages in LOG2 UNITS, as the GPU kernels keep them (ldpc-sims_amd/csrc/common.h): s2 = fma(L, log2 e, sum2),
  * a = exp2(-|s2|), the check output log2(S/D) clamped to [0, cmax2] with cmax2 = min(fp32(clamp * log2 e), 24 =
  * fp32(log2 RMAX)), z = fma(sum2, fp32(ln 2 / 2), 0.5 * L).  The trace reports messages in natural units (x ln 2). */
@@ -98,7 +101,11 @@ static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float 
         return;
     }
     uint32_t sg = 0;
-    for (int t = 0; t < d; ++t) sg ^= f2u(sa[t]);
+    int n1 = 0;  /* edges with a == 1 */
+    for (int t = 0; t < d; ++t) {
+        sg ^= f2u(sa[t]);
+        n1 += fabsf(sa[t]) == 1.0f;
+    }
     sufD[d - 1] = fabsf(sa[d - 1]);
     sufS[d - 1] = 1.0f;
     for (int t = d - 2; t >= 1; --t) {
@@ -115,6 +122,7 @@ static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float 
         float y = log2f(S / D);   /* D == 0 (every other a underflowed): +inf -> the ceiling */
         if (!(y >= 0.0f)) y = 0.0f;  /* S >= D: a ratio rounded below 1 is log 1 */
         if (y > cmax2) y = cmax2;
+        if (n1 - (fabsf(sa[t]) == 1.0f) > 0) y = 0.0f;  /* another edge has a == 1: the reference's p = 0 */
         out[t] = u2f(f2u(y) | ((sg ^ f2u(sa[t])) & 0x80000000u));
         const float a = fabsf(sa[t]);
         const float nD = fmaf(a, pS, pD), nS = fmaf(a, pD, pS);

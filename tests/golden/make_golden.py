@@ -36,11 +36,13 @@ What it records (all .npz, numeric arrays only — loadable with allow_pickle=Fa
   * e2e_quantized.npz      the reference's quantized chain (3-bit ADC via gen_qdata, evaluate_quantized.py) into
                            decode_bits at clamp 20: (64,32) at 3 iterations, (648,1/2) at 50; LLRs with exact
                            zeros (e2eq).
+  * bp_zeros.npz           clustered exact-zero LLRs (2-3 zeros in a third of the checks, both signs): (64,32) and
+                           (648,1/2), 1/2/3/5 iterations, clamp 10 and 20, p1 and z, fp32 and .double() (zeros).
   * bp_wifi648_12_sp_it50_cl20.npz  (648,1/2) 50 iterations at clamp 20, above the p-clamp ceiling; plus
                            (wificlampb32) the reference's .double() module with the fp32 module's p-clamp bound
                            swapped in at run time (f32_pclamp): p1_f64b32_* / z_f64b32_*.
 
-    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32] [wifi1944c2] [e2e648] [e2eq]
+    python tests/golden/make_golden.py [bp] [adc] [weighted] [wifi] [x0] [wifilong] [wificlamp] [wificlampb32] [wifi1944c2] [e2e648] [e2eq] [zeros]
 """
 import contextlib
 import os
@@ -557,12 +559,52 @@ def gen_x0():
     np.savez_compressed(os.path.join(HERE, "bp_x0.npz"), clamp=10.0, **rec)
 
 
+def gen_zeros():
+    """bp_zeros.npz: LLRs with CLUSTERED exact zeros (erasures): in a third of the checks, two or three of the
+    check's variables get an LLR of exactly +0 or -0, the rest BPSK/AWGN values at 2 dB — the s = +-0 case of the
+    first VC layer (bp_vc.py:27 gives tanh(0) = 0, so bp_cv.py's product is exactly 0 for every other edge of such
+    a check) with several zeros per check row and per variable.  (64,32) and (648,1/2), 1 / 2 / 3 / 5 iterations,
+    clamp 10 and 20, the fp32 module and .double(): p1 and z (run_ref_z)."""
+    from ldpc_amd.codes import get_code
+    rec = {}
+    for name, B in (("peg64_32", 64), ("wifi648_12", 16)):
+        H = parity.H.astype(np.int64) if name == "peg64_32" else np.asarray(get_code(name)[0], np.int64)
+        m, n = H.shape
+        enc = Encoder(H)
+        rng = np.random.default_rng(7070 + n)
+        cw = enc.encode(rng.integers(0, 2, size=(B, enc.k)))
+        llr = bpsk_awgn_llr(cw.astype(np.float64), 2.0, enc.k / n, rng)
+        nz = 0
+        for b in range(B):
+            for c in rng.choice(m, size=m // 3, replace=False):
+                cols = np.flatnonzero(H[c])
+                for v in rng.choice(cols, size=min(len(cols), int(rng.integers(2, 4))), replace=False):
+                    llr[b, v] = np.float32(-0.0) if rng.random() < 0.5 else np.float32(0.0)
+                    nz += 1
+        rec[f"{name}_llr"] = llr
+        rec[f"{name}_codeword"] = cw.astype(np.uint8)
+        for iters in (1, 2, 3, 5):
+            for clamp in (10.0, 20.0):
+                tag = f"{name}_it{iters}_cl{int(clamp)}"
+                p32, z32 = run_ref_z(H, iters, clamp, llr)
+                p64, z64 = run_ref_z(H, iters, clamp, llr, double=True)
+                rec[f"{tag}_p1_f32"] = p32.astype(np.float32)
+                rec[f"{tag}_z_f32"] = z32.astype(np.float32)
+                rec[f"{tag}_p1_f64"] = p64
+                rec[f"{tag}_z_f64"] = z64
+                print("zeros", tag, "zero LLRs", int((llr == 0).sum()), "exact-zero z (f32/f64):",
+                      int((z32 == 0).sum()), int((z64 == 0).sum()), "bit errors:",
+                      int((np.round(p32) != cw).sum()), flush=True)
+    np.savez_compressed(os.path.join(HERE, "bp_zeros.npz"), **rec)
+
+
 if __name__ == "__main__":
     parts = sys.argv[1:] or ["bp", "adc", "weighted", "wifi", "x0", "wifilong", "wificlamp", "wificlampb32",
-                             "wifi1944c2", "e2e648", "e2eq"]
+                             "wifi1944c2", "e2e648", "e2eq", "zeros"]
     for part in parts:
         {"bp": gen_bp, "adc": gen_adc, "weighted": gen_weighted, "wifi": gen_wifi_sp, "x0": gen_x0,
          "wifilong": gen_wifi_sp_long,
          "wificlamp": lambda: gen_wifi_sp_long(WIFI_SP_CLAMPS, clamp_tag=True),
-         "wificlampb32": gen_wifi_clamp_f32bound, "wifi1944c2": gen_wifi1944_c2, "e2e648": gen_e2e648, "e2eq": gen_e2e_quantized}[part]()
+         "wificlampb32": gen_wifi_clamp_f32bound, "wifi1944c2": gen_wifi1944_c2, "e2e648": gen_e2e648, "e2eq": gen_e2e_quantized,
+         "zeros": gen_zeros}[part]()
     print("done")

@@ -676,3 +676,46 @@ def test_decode_bits_dropin_long_reference_goldens(name, iters):
         assert out.dtype == np.float64
         assert np.array_equal(out[:rows], np.round(d[f"p1_f32_{tag}"][:rows]).astype(np.float64))
         assert not out[rows:].any()
+
+
+@pytest.mark.parametrize("code", ["peg64_32", "wifi648_12"])
+def test_clustered_zero_llrs_vs_reference_golden(code):
+    """Clustered exact-zero LLRs through the reference (tests/golden/bp_zeros.npz, 1/2/3/5 iterations, clamp 10
+    and 20): the GPU (the register kernel's a == 1 pass on (648,1/2), the generic kernels on both) meets the
+    reference as the oracle does (softparity.check_zeros_golden: exact zeros where the reference's are, its
+    fp32 bits outside the rounding band), and the kernel families agree bit for bit."""
+    from softparity import check_zeros_golden
+    d = np.load(os.path.join(GOLDEN, "bp_zeros.npz"))
+    H = np.asarray(get_code(code)[0])
+    dec = ldpc_amd.get_decoder(H)
+    x = torch.from_numpy(d[f"{code}_llr"]).cuda()
+    for it in (1, 2, 3, 5):
+        for cl in (10, 20):
+            tag = f"{code}_it{it}_cl{cl}"
+            a = dec.decode(x, it, algo="tanh", clamp=float(cl), soft="z")
+            g = dec.decode(x, it, algo="tanh", clamp=float(cl), soft="z", force_generic=True)
+            assert torch.equal(a["bits"], g["bits"]) and torch.equal(a["soft"].view(torch.int32), g["soft"].view(torch.int32)), tag
+            check_zeros_golden(f"gpu zeros {code}", a["bits"].cpu().numpy(), a["soft"].cpu().numpy(), d, tag)
+
+
+@pytest.mark.parametrize("code,early", [("wifi648_12", True), ("wifi1296_23", False), ("wifi1296_23", True),
+                                        ("wifi1944_56", False), ("wifi1944_56", True)])
+def test_zero_llr_pass_equals_generic_bitwise(code, early):
+    """Every tanh-SP register kernel's a == 1 pass (PASS 2: the waves / units whose LLRs hold an exact zero)
+    against the generic kernels bit for bit — bits, z and iteration counts — on a batch where about half the
+    codewords carry erasures (so both passes of one launch write outputs), fixed count and early stop."""
+    H = np.asarray(get_code(code)[0])
+    dec = ldpc_amd.get_decoder(H)
+    rate = 1 - H.shape[0] / H.shape[1]
+    _, x = _llr(H, 37, 3.0, seed=17, rate=rate)
+    rng = np.random.default_rng(5)
+    er = rng.random(x.shape) < 0.04
+    er[::2] = False                                   # even rows: no erasure (the plain pass)
+    x[er] = 0.0
+    xt = torch.from_numpy(x).cuda()
+    kw = dict(algo="tanh", clamp=20.0, soft="z", early_stop=early, want_iters=True)
+    a = dec.decode(xt, 20, **kw)
+    g = dec.decode(xt, 20, force_generic=True, **kw)
+    assert torch.equal(a["bits"], g["bits"])
+    assert torch.equal(a["soft"].view(torch.int32), g["soft"].view(torch.int32))
+    assert torch.equal(a["iters_used"], g["iters_used"])

@@ -297,3 +297,21 @@ def test_zero_llr_rows_give_exact_zero_in_both_forms():
     b = oracle.sp_f32(H, llr, 10, 10.0, stable=True)
     assert np.array_equal(a["bits"], b["bits"])
     assert np.allclose(a["z"], b["z"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("code", ["peg64_32", "wifi648_12"])
+def test_oracle_clustered_zero_llrs_golden(code):
+    """Clustered exact-zero LLRs through the reference (tests/golden/bp_zeros.npz: 2-3 zeros of both signs in a
+    third of the checks, 1/2/3/5 iterations, clamp 10 and 20): the oracle's (D, S) form gives exact zeros where
+    the reference does (an edge whose exclusive set holds an a == 1 edge outputs +-0, cn_stable_f32) and the
+    reference's fp32 bits outside the rounding band (softparity.check_zeros_golden).  Before the rule the fma
+    join left ulp-sized outputs there and flipped 1-6 hard decisions."""
+    from softparity import check_zeros_golden
+    from ldpc_amd.codes import get_code
+    d = np.load(os.path.join(GOLDEN, "bp_zeros.npz"))
+    H = np.asarray(get_code(code)[0])
+    x = d[f"{code}_llr"]
+    for it in (1, 2, 3, 5):
+        for cl in (10, 20):
+            r = oracle.sp_f32(H, x, it, float(cl), stable=True)
+            check_zeros_golden(f"oracle-ds zeros {code}", r["bits"], r["z"], d, f"{code}_it{it}_cl{cl}")

@@ -51,6 +51,13 @@ constexpr int nz_max() {
 // buffer).  QC_SL_SP_L: where L lives — 0 VGPRs, 1 LDS, 2 re-read from global memory (an L2 hit) at every
 // use.  Fixed-count kernel: one buffer + L in global = 26 KB of LDS per unit, 112 VGPRs: five units
 // (15 waves) per CU instead of two.
+#ifndef QC_SL_POS_STRIDE
+// lane l of slot wave k holds frame position S*l + k (1) instead of l + ZL*k (0): a rotation by c reads positions
+// (S*l + k + c) mod Z = S*((l + q) mod ZL) + r, whose LDS banks (a/4 mod 32) are distinct for odd S, so no access
+// of the rotated-circulant slots conflicts; with contiguous positions every window that wraps past Z conflicted
+// (round 4: SQ_LDS_BANK_CONFLICT 21 % of the resident kernel's LDS cycles).  A relabelling: bitwise the same.
+#define QC_SL_POS_STRIDE 1
+#endif
 #ifndef QC_SL_IDLE_ALIAS
 #define QC_SL_IDLE_ALIAS 1  // idle lanes read at their wave's first position (0: at position 0, round 2)
 #endif
@@ -109,7 +116,8 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     // served per 32-lane half with bank = (address / 4) mod 32, and aliased to position 0 (round 2) the idle
     // lanes of waves k = 1, 2 read a distinct address on a bank their active lanes use — one extra LDS cycle
     // per read; repeating an active lane's address of their own wave is a broadcast instead.
-    const int zc = live ? l + ZL * k : (QC_SL_IDLE_ALIAS ? ZL * k : 0);
+    const int p0 = QC_SL_POS_STRIDE ? k : ZL * k;  // this wave's first position
+    const int zc = live ? (QC_SL_POS_STRIDE ? S * l + k : l + ZL * k) : (QC_SL_IDLE_ALIAS ? p0 : 0);
     const int xb = h * 2 * Z + zc;           // this lane's position in an exchange row
     // L = -llr (bp.py:47) of this lane's variable in every block column
     const float* const lp = llr + (valid ? cw * N : 0);
@@ -432,7 +440,8 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
     // idle lanes read at their wave's first position (a broadcast, see k_qc_sp_sl) and never store; with
     // QC_RS_IDLE_DUP they shadow lane l - ZL instead — the same loads, so the same values, written to the same
     // slots by the same instruction — and the stores need no exec mask
-    const int zc = live ? l + ZL * k : (QC_RS_IDLE_DUP ? l - ZL + ZL * k : ZL * k);
+    auto pos_of = [&](int ll) { return QC_SL_POS_STRIDE ? S * ll + k : ll + ZL * k; };  // see QC_SL_POS_STRIDE
+    const int zc = live ? pos_of(l) : (QC_RS_IDLE_DUP ? pos_of(l - ZL) : pos_of(0));
     const bool store = QC_RS_IDLE_DUP ? true : live;
     // byte addresses of this lane's slot for a = 0 .. NA-1 (check side) and b = 0 .. Q-1 (variable side)
     int aC[NA], aV[Q];
@@ -617,17 +626,25 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
         });
         __syncthreads();
     }
-    if (valid) {
+    // the output's lane coordinates recomputed after the loop — the lane id by v_mbcnt (the work-item id VGPR of
+    // the launch is long gone), the slot wave k is scalar — instead of kept across it: the values set before the
+    // loop and read after it went to scratch (round 4: 63 MB of scratch stores per launch, WRITE_SIZE 1.92x the
+    // bits out)
+    const int lane_e = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const int le = lane_e & 31, he = (lane_e >> 5) & 1;
+    const int64_t cwe = (int64_t)blockIdx.x * 2 + he;
+    if (le < ZL && cwe < B) {
+        const int zce = pos_of(le);
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
             constexpr int j = decltype(jj)::value;
             const float zz = zsum(jj);
-            int t = zc + C::PHI[j];
+            int t = zce + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
-            const int64_t o = cw * N + j * Z + t;
+            const int64_t o = cwe * N + j * Z + t;
             if (bits) bits[o] = (uint8_t)Num<float>::bit(zz);
             if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
         });
-        if (k == 0 && l == 0 && iters_used) iters_used[cw] = iters;
+        if (k == 0 && le == 0 && iters_used) iters_used[cwe] = iters;
     }
 }
 

@@ -1,9 +1,9 @@
 """Every kernel a BASELINE.json configuration dispatches is spill-free: no VGPR spills and no scratch, read
 from the gfx950 code objects' AMDGPU metadata notes of the built libldpc_hip.so (no GPU needed;
 scripts/kernel_resources.py).  SGPR spills go to VGPR lanes (v_writelane), not to memory, and are allowed.
-One exception, checked on the disassembly instead: config [2]'s resident kernel keeps a few values set before
-its iteration loop and read after it in scratch (one-block check rows, qc_sl_sp.h QC_RS_DS_BLOCK) — no scratch
-access inside the loop.  The tanh-SP register kernels come in two passes (qc.hip / qc_sl_sp.h PASS): the plain
+Config [2]'s resident kernel is checked on the disassembly as well: no scratch anywhere (round 4 kept five values
+set before its iteration loop and read after it in scratch — 63 MB of stores per launch; its epilogue now
+recomputes them, the lane id by v_mbcnt).  The tanh-SP register kernels come in two passes (qc.hip / qc_sl_sp.h PASS): the plain
 loop (PASS 1) every input without an exact-zero LLR runs, checked here, and the a == 1 rule's loop (PASS 2) for the
 waves / units whose LLRs hold an exact zero (erasures, quantized LLRs), which may spill: it runs only there.
 
@@ -37,8 +37,8 @@ BASELINE_KERNELS = [
     r"k_final<float, 32, (true|false)>",
     r"k_qc_sp_st<ldpc::Wifi648_12, false, 1>",
 ]
-MAX_SPILL_OUTSIDE_LOOP = {r"k_qc_sp_rs<ldpc::Wifi1944_56, 1>": 8}
-MAX_SCRATCH_IN_LOOP = 5
+MAX_SPILL_OUTSIDE_LOOP = {r"k_qc_sp_rs<ldpc::Wifi1944_56, 1>": 0}
+MAX_SCRATCH_IN_LOOP = 0
 
 
 @pytest.fixture(scope="module")
@@ -77,8 +77,6 @@ def test_resident_kernel_spills_only_outside_the_iteration_loop(resources, patte
     loop = main_loop(lines)
     assert len(loop) > 1000, len(loop)
     scratch = [op for _, op, _, _ in loop if op.startswith("scratch_")]
-    # the five values set before the loop and read after it: saved / restored at the loop head since the two
-    # PASS kernels (a handful against ~3,500 instructions per iteration); nothing in the phases themselves
     assert len(scratch) <= MAX_SCRATCH_IN_LOOP, scratch
 
 

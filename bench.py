@@ -127,7 +127,7 @@ def main():
     total_cw = world * args.steps * B
     ranks = rank_evidence(world, rank, local, my_elapsed)
     value = total_cw / elapsed
-    roof = roofline(n, E, B, gpu_ms, args, wl.kpath, wl.m)
+    roof = roofline(n, E, B, gpu_ms, args, wl.kpath, wl.m, wl.mean_iters)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # CPU baseline at N=1 only
@@ -218,7 +218,8 @@ def run_leg(name, args, rank, local, world):
     rec = {"baseline_config": LEGS[name]["baseline"], "value": world * steps * wl.B / elapsed,
            "unit": "codewords/s", "n_gpus": world, "steps": steps, "warmup": 1,
            "ms_per_step": elapsed / steps * 1e3, "ms_per_launch": gpu_ms,
-           "config": wl.config_dict(world), "roofline": roofline(wl.n, wl.E, wl.B, gpu_ms, la, wl.kpath, wl.m), "ber": ber}
+           "config": wl.config_dict(world), "roofline": roofline(wl.n, wl.E, wl.B, gpu_ms, la, wl.kpath, wl.m, wl.mean_iters),
+           "mean_iters": wl.mean_iters, "ber": ber}
     if world > 1:
         rec["ranks"] = rank_evidence(world, rank, local, my_elapsed)
     wl.free()
@@ -281,10 +282,11 @@ class Workload:
         self.ws = torch.empty((max(self.wsb, 1),), dtype=torch.uint8, device="cuda")
         self.bits = torch.empty((B, n), dtype=torch.uint8, device="cuda")
 
-    def step(self, x):
+    def step(self, x, used=None):
         from ldpc_amd import _abi
         _abi.check(self.lib.ldpc_decode_ex(self.dec._h, x.data_ptr(), self.B, self.p, self.bits.data_ptr(), None,
-                                           None, self.ws.data_ptr(), self.wsb, self.stream.cuda_stream))
+                                           used.data_ptr() if used is not None else None, self.ws.data_ptr(), self.wsb,
+                                           self.stream.cuda_stream))
 
     def ber(self):
         """Untimed pass over every point: error counts on device, summed over ranks (the one collective)."""
@@ -292,12 +294,19 @@ class Workload:
         from ldpc_amd import _abi
         from ldpc_amd.dist import allreduce_counts
         counts = torch.zeros((len(self.ebn0), 3), dtype=torch.int64, device="cuda")
+        # with early stop, the iterations each codeword ran: their mean over the grid (the timed loop cycles over the
+        # same points) is the byte model's iteration count
+        used = torch.empty((self.B,), dtype=torch.int32, device="cuda") if self.args.early_stop else None
+        used_sum = torch.zeros((), dtype=torch.int64, device="cuda")
         for i in range(len(self.ebn0)):
-            self.step(self.llrs[i])
+            self.step(self.llrs[i], used)
+            if used is not None:
+                used_sum += used.sum()
             _abi.check(self.lib.ldpc_count_errors(self.bits.data_ptr(), self.cw.data_ptr(), self.B, self.n, self.k,
                                                   counts[i].data_ptr(), self.stream.cuda_stream))
         allreduce_counts(counts)  # 24 B x points per rank (RCCL)
         c = counts.cpu().numpy().astype(np.float64)
+        self.mean_iters = (float(used_sum.item()) / (self.B * len(self.ebn0))) if used is not None else float(self.args.iters)
         return {"ebn0_db": self.ebn0.tolist(), "coded_ber_info": (c[:, 0] / (c[:, 2] * self.k)).tolist(),
                 "coded_bler": (c[:, 1] / c[:, 2]).tolist(), "codewords_per_point": int(c[0, 2])}
 
@@ -377,7 +386,7 @@ def ira_bytes_per_cw(n, m, iters):
     return iters * (12 * n + 36 * m) + 21 * n + 24 * m
 
 
-def roofline(n, E, B, launch_ms, args, kpath, m=None):
+def roofline(n, E, B, launch_ms, args, kpath, m=None, iters=None):
     """The decode launch against the resource that binds it.
 
     * Streaming (generic CSR) kernels move every message through HBM each iteration: bound "hbm",
@@ -392,7 +401,8 @@ def roofline(n, E, B, launch_ms, args, kpath, m=None):
       measured PMC traffic.
     """
     s_b = 1 if args.algo in ("qminsum", "qms") else 4  # SURVEY §8(d): 5-bit mode s_m = s_L = 1 byte
-    bpc = algorithmic_bytes_per_cw(n, E, args.iters, s_b, s_b)
+    it = args.iters if iters is None else iters  # early stop: the mean iterations executed (SURVEY §8(d))
+    bpc = algorithmic_bytes_per_cw(n, E, it, s_b, s_b)
     launch_s = launch_ms * 1e-3
     model_gbps = bpc * B / launch_s / 1e9
     rec = None
@@ -409,7 +419,7 @@ def roofline(n, E, B, launch_ms, args, kpath, m=None):
             note = "no counter record for this Eb/N0 grid and seed (early-stop work depends on the data)"
     c = rec["counters_per_launch"] if rec else {}
     hbm_bytes = rec["derived"].get("hbm_bytes") if rec else None
-    hbm = {"model_bytes_per_codeword": bpc, "model_GBps": model_gbps, "model_frac": model_gbps / HBM_PEAK_GBPS,
+    hbm = {"model_bytes_per_codeword": bpc, "model_iters": it, "model_GBps": model_gbps, "model_frac": model_gbps / HBM_PEAK_GBPS,
            "traffic_bytes_per_launch": hbm_bytes,
            "traffic_GBps": hbm_bytes / launch_s / 1e9 if hbm_bytes else None,
            "traffic_frac": hbm_bytes / launch_s / 1e9 / HBM_PEAK_GBPS if hbm_bytes else None}

@@ -89,6 +89,49 @@ namespace ldpc {
 template <bool EARLY>
 constexpr int pk_tpb() { return EARLY ? QC_PK_TPB_EARLY : QC_PK_TPB; }
 
+// QC_PK_ILV (one codeword pair per wave, even Z: (1296,2/3), config [3]): lifting index z lives in lane
+// (z & 1) * 32 + z / 2 — even z in the lower half, odd in the upper — instead of lane z.  ds_bpermute serves a
+// wave in two 32-lane halves with bank = source lane mod 32; with z in lane z every rotation whose source window
+// wraps past Z puts two sources of one half on a bank (round 4: SQ_LDS_BANK_CONFLICT 19 % of the kernel's LDS
+// cycles).  Interleaved, a rotation by rho = 2v + f reads, for the half of parity e, the half of parity e ^ f at
+// lane index (u + v + f e) mod Z/2: distinct lanes of one half, so every rotation is conflict-free.  The early-stop
+// ballots are permuted the same way (ilv_rot).  A relabelling of lanes: bitwise the same results.
+#ifndef QC_PK_ILV
+#define QC_PK_ILV 1
+#endif
+template <int Z>
+constexpr int ilv_u(int l) {  // a lane's index within its half; an idle lane (index >= Z/2) that of the lane it aliases
+    return (l & 31) < Z / 2 ? (l & 31) : ((l & 31) - Z / 2) % (Z / 2);
+}
+template <int Z>
+constexpr uint64_t ilv_active() {
+    uint64_t m = 0;
+    for (int l = 0; l < 64; ++l) m |= ((l & 31) < Z / 2 ? 1ull : 0ull) << l;
+    return m;
+}
+// lanes whose source lane index of rotation RHO passes Z/2 (they take the wrapped address)
+template <int Z, int RHO>
+constexpr uint64_t ilv_wrap_mask() {
+    uint64_t m = 0;
+    for (int l = 0; l < 64; ++l) {
+        const int e = l >> 5, u = ilv_u<Z>(l);
+        if (u + (RHO >> 1) + ((RHO & 1) ? e : 0) >= Z / 2) m |= 1ull << l;
+    }
+    return m;
+}
+// bit l of the result = bit lane((z(l) + S) mod Z) of x (the interleaved counterpart of qc_common.h rot_lanes):
+// an even S rotates each half's Z/2-bit field by S/2; an odd S swaps the halves, the lower (even z) taking the
+// upper field rotated by (S-1)/2 and the upper the lower rotated by (S+1)/2.  Bits outside the fields: garbage.
+template <int Z, int S>
+__device__ __forceinline__ uint64_t ilv_rot(uint64_t x) {
+    constexpr int H = Z / 2;
+    auto r = [](uint32_t y, int k) { return k == 0 ? y : ((y >> k) | (y << (H - k))); };
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if constexpr (S == 0) return x;
+    else if constexpr (S % 2 == 0) return ((uint64_t)r(hi, S / 2) << 32) | r(lo, S / 2);
+    else return ((uint64_t)r(lo, (S + 1) / 2 % H) << 32) | r(hi, S / 2);
+}
+
 using h2 = _Float16 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h2 as_h2(uint32_t x) { return __builtin_bit_cast(h2, x); }
 __device__ __forceinline__ uint32_t as_u(h2 x) { return __builtin_bit_cast(uint32_t, x); }
@@ -170,14 +213,21 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     static_assert((1 + max_col_deg<C>()) * 127 < 2048, "fp16 must hold every posterior exactly");
     static_assert(min_row_deg<C>() >= 2, "check degree >= 2");
     constexpr int CPW = (Z <= 32) ? 2 : 1;
+    constexpr bool LDSROT = EARLY ? QC_PK_LDSROT_EARLY : QC_PK_LDSROT;
+    constexpr bool DROT = EARLY ? QC_PK_DROT_EARLY : QC_PK_DROT;
+    constexpr bool ILV = QC_PK_ILV && CPW == 1 && Z % 2 == 0 && !LDSROT && !DROT;
     const int lane = threadIdx.x & 63;
     const int half = (CPW == 2) ? (lane >> 5) : 0;
-    const int z = (CPW == 2) ? (lane & 31) : lane;
+    // lifting index of this lane (>= Z: idle); ILV: even z in the lower half, odd in the upper
+    const int z = ILV ? ((lane & 31) < Z / 2 ? 2 * (lane & 31) + (lane >> 5) : Z + (lane & 31)) : ((CPW == 2) ? (lane & 31) : lane);
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t cw0 = (wave * CPW + half) * 2;  // low fp16: cw0, high: cw0 + 1
     const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
+    // ILV rotation bases: even rotations read this half at index u + v, odd ones the other half at u + e + v
+    const int ue = ILV ? 32 * (lane >> 5) + ((lane & 31) < Z / 2 ? (lane & 31) : ((lane & 31) - Z / 2) % (Z / 2)) : 0;
+    const int bE = 4 * ue, bO = 4 * ((ue ^ 32) + (lane >> 5));
     using f4 = __attribute__((ext_vector_type(4))) float;
     constexpr int LSTR = lstr<C>();
     __shared__ __attribute__((aligned(16))) uint32_t Ls[pk_tpb<EARLY>() * LSTR];  // lane-major packed L rows (lpos)
@@ -185,7 +235,6 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     const int lrow4 = lrow * 4;  // bytes (lds_reload)
 
     // lane rotations through a per-wave LDS row (as k_qc_ms_ph, qc.hip QC_PH_LDSROT) or ds_bpermute
-    constexpr bool LDSROT = EARLY ? QC_PK_LDSROT_EARLY : QC_PK_LDSROT;
     __shared__ uint32_t Rw[LDSROT ? pk_tpb<EARLY>() : 1];
     const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;
     const int rb4 = base4 + wrow, rb4m = base4m + wrow;
@@ -202,13 +251,22 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
         }
     };
     constexpr int MINU = (Z <= 32) ? QC_PK_ADDR_MIN_USES : QC_PK_ADDR_MIN_USES_Z64;
+    // byte address of "the value of lifting index (z + rho) mod Z" for ds_bpermute
+    auto raddr = [&](auto rr) __attribute__((always_inline)) {
+        constexpr int rho = decltype(rr)::value;
+        if constexpr (ILV) {
+            constexpr int v = rho >> 1;
+            if constexpr (rho & 1) return sel_lanes<ilv_wrap_mask<Z, rho>()>(bO, bO - 2 * Z) + 4 * v;
+            else return sel_lanes<ilv_wrap_mask<Z, rho>()>(bE, bE - 2 * Z) + 4 * v;
+        } else {
+            return sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho;
+        }
+    };
     int ra[Z];
     static_for<1, Z>([&](auto rr) __attribute__((always_inline)) {
         constexpr int rho = decltype(rr)::value;
-        if constexpr (rot_uses<C>(rho) >= MINU && !(EARLY ? QC_PK_DROT_EARLY : QC_PK_DROT))
-            ra[rho] = sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho;
+        if constexpr (rot_uses<C>(rho) >= MINU && !DROT) ra[rho] = raddr(rr);
     });
-    constexpr bool DROT = EARLY ? QC_PK_DROT_EARLY : QC_PK_DROT;
     constexpr int DW = CPW * 2 * Z + 64 + 2 * Z;  // words per wave: doubled rows, then the idle lanes' stretch
     __shared__ uint32_t Rd[DROT ? (pk_tpb<EARLY>() / 64) * DW : 1];
     const int da = DROT ? 4 * ((int)(threadIdx.x >> 6) * DW + ((z < Z) ? half * 2 * Z + z : CPW * 2 * Z + lane)) : 0;
@@ -225,7 +283,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
         } else if constexpr (rot_uses<C>(rho) >= MINU) {
             return xfer(ra[rho], x);
         } else {
-            return xfer(sel_lanes<wrap_mask<Z, CPW>(Z - rho)>(rb4, rb4m) + 4 * rho, x);
+            return xfer(raddr(rr), x);
         }
     };
     (void)ra;
@@ -319,8 +377,13 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     };
 
     // early stop: codeword k of this wave = (group g, fp16 half p), k = 2g + p; converged ones park APP
-    constexpr uint64_t ACTIVE = lane_range_mask<Z, CPW>(0, Z);
-    constexpr uint64_t G0 = lane_range_mask<Z, 1>(0, Z), G1 = (CPW == 2) ? (G0 << 32) : 0;
+    constexpr uint64_t ACTIVE = ILV ? ilv_active<Z>() : lane_range_mask<Z, CPW>(0, Z);
+    constexpr uint64_t G0 = ILV ? ilv_active<Z>() : lane_range_mask<Z, 1>(0, Z), G1 = (CPW == 2) ? (G0 << 32) : 0;
+    auto lrot = [&](auto ss, uint64_t b) __attribute__((always_inline)) {  // lane-mask rotation (early stop)
+        constexpr int S = decltype(ss)::value;
+        if constexpr (ILV) return ilv_rot<Z, S>(b);
+        else return rot_lanes<Z, CPW, S>(b);
+    };
     constexpr uint32_t ALL = (CPW == 2) ? 0xfu : 0x3u;
     uint32_t done = 0;  // bit k: codeword k converged
     int used0 = iters, used1 = iters, used2 = iters, used3 = iters;
@@ -363,7 +426,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
                             static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
                                 constexpr int t = decltype(tt)::value;
                                 const uint64_t b = __ballot(as_h2(app[C::COL[r][t]])[k] < (_Float16)0) & ACTIVE;
-                                par ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                                par ^= lrot(std::integral_constant<int, C::SHR[r][t]>{}, b);
                             });
                             if (par & G0) conv &= ~(1u << k);
                         });
@@ -382,7 +445,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
                         static_for<0, MB>([&](auto rr) __attribute__((always_inline)) {
                             constexpr int r = decltype(rr)::value;
                             constexpr int t = first_slot<C>(r, j);
-                            if constexpr (t >= 0) par[r] ^= rot_lanes<Z, CPW, C::SHR[r][t]>(b);
+                            if constexpr (t >= 0) par[r] ^= lrot(std::integral_constant<int, C::SHR[r][t]>{}, b);
                         });
                     });
                     uint64_t u = 0;
@@ -425,7 +488,8 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     if (!early_exit && iters > 0) cn_phase();
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    const int zo = (CPW == 2) ? (tid & 31) : (tid & 63);
+    const int zo = ILV ? ((tid & 31) < Z / 2 ? 2 * (tid & 31) + ((tid >> 5) & 1) : Z + (tid & 31))
+                       : ((CPW == 2) ? (tid & 31) : (tid & 63));
     const int go = (CPW == 2) ? ((tid >> 5) & 1) : 0;
     const int64_t c0 = ((((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + go) * 2;
     const bool park0 = EARLY && ((done >> (2 * go)) & 1u), park1 = EARLY && ((done >> (2 * go + 1)) & 1u);

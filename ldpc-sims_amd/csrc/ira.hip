@@ -112,13 +112,17 @@ __device__ __forceinline__ float ira_vn_info(const int32_t* __restrict__ row, in
 
 // One task = one variable group (information group g < G, or parity row a = g - G) of one codeword; lanes =
 // the 360 positions.  Writes app in the permuted layout (information: g*360 + m, parity: k + a*360 + b).
+// A workgroup runs `tpw` consecutive tasks of its codeword (fewer, longer-lived waves; LDPC_IRA_TPW).
 template <int MAXDV>
 __global__ __launch_bounds__(384) void k_ira_vn(IRADev t, const float* __restrict__ L, float* __restrict__ app,
-                                                const float2* __restrict__ S, const uint32_t* __restrict__ MT, int Bc) {
-    int cw, gi;
-    if (!ira_task(t.G + t.q, Bc, cw, gi)) return;
+                                                const float2* __restrict__ S, const uint32_t* __restrict__ MT, int Bc,
+                                                int tpw) {
+    const int T = t.G + t.q;
+    int cw, tb;
+    if (!ira_task((T + tpw - 1) / tpw, Bc, cw, tb)) return;
     const int pos = threadIdx.x;
     if (pos >= kIZ) return;
+    for (int gi = tb * tpw; gi < T && gi < (tb + 1) * tpw; ++gi) {
     const int64_t vo = (int64_t)cw * t.n + (int64_t)gi * kIZ + pos;
     const int64_t so = (int64_t)cw * t.M;
     float a = L[vo];
@@ -145,17 +149,20 @@ __global__ __launch_bounds__(384) void k_ira_vn(IRADev t, const float* __restric
         }
     }
     app[vo] = a;
+    }
 }
 
 // One task = one check row a of one codeword; lanes = positions b.  Reads the posteriors of the row's
 // variables and its own state, writes the new state (the oracle's k_cn_ms arithmetic on v2c = app - c2v).
 template <int MAXR>
 __global__ __launch_bounds__(384) void k_ira_cn(IRADev t, const float* __restrict__ app, float2* __restrict__ S,
-                                                uint32_t* __restrict__ MT, int Bc, float clamp, float alpha, float beta) {
-    int cw, ra;
-    if (!ira_task(t.q, Bc, cw, ra)) return;
+                                                uint32_t* __restrict__ MT, int Bc, float clamp, float alpha, float beta,
+                                                int tpw) {
+    int cw, tb;
+    if (!ira_task((t.q + tpw - 1) / tpw, Bc, cw, tb)) return;
     const int pos = threadIdx.x;
     if (pos >= kIZ) return;
+    for (int ra = tb * tpw; ra < t.q && ra < (tb + 1) * tpw; ++ra) {
     const int64_t ao = (int64_t)cw * t.n;
     const int64_t si = (int64_t)cw * t.M + (int64_t)ra * kIZ + pos;
     const float2 st = S[si];
@@ -209,6 +216,7 @@ __global__ __launch_bounds__(384) void k_ira_cn(IRADev t, const float* __restric
     if (has_prev) meta |= ((sgn ^ f2u(vp1)) >> 31) << (kIPS + 1);
     S[si] = make_float2(mag1, mag2);
     MT[si] = meta;
+    }
 }
 
 // natural [B][n] llr -> permuted L = -llr: information part as is, parity block [360][q] (index b*q + a)
@@ -402,6 +410,8 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     const IRADev t{s->vn, s->vdeg, s->cn, s->cdeg, s->q, s->G, s->k, s->n, s->M};
     const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
     const unsigned tiles = (unsigned)((s->k + 1023) / 1024 + ((kIZ + 63) / 64) * ((s->q + 63) / 64));
+    const char* tenv = getenv("LDPC_IRA_TPW");  // tasks per workgroup (A/B knob)
+    const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 1;
     for (int64_t o = 0; o < B; o += bc) {
         const int b = (int)(B - o < bc ? B - o : bc);
         const int64_t vo = o * s->n;
@@ -410,13 +420,13 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
         if (hipMemsetAsync(S, 0, (size_t)b * s->M * 8, st) != hipSuccess ||
             hipMemsetAsync(MT, 0, (size_t)b * s->M * 4, st) != hipSuccess)
             return set_error(LDPC_EHIP, "IRA state init failed");
-        const unsigned gvn = cw8 * (unsigned)(s->G + s->q), gcn = cw8 * (unsigned)s->q;
+        const unsigned gvn = cw8 * (unsigned)((s->G + s->q + tpw - 1) / tpw), gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
         for (int it = 0; it <= p.iters; ++it) {
-            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, 384, 0, st>>>(t, L, app, S, MT, b);
-            else k_ira_vn<16><<<gvn, 384, 0, st>>>(t, L, app, S, MT, b);
+            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, 384, 0, st>>>(t, L, app, S, MT, b, tpw);
+            else k_ira_vn<16><<<gvn, 384, 0, st>>>(t, L, app, S, MT, b, tpw);
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
-            if (s->maxr <= 8) k_ira_cn<8><<<gcn, 384, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta);
-            else k_ira_cn<kICS><<<gcn, 384, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta);
+            if (s->maxr <= 8) k_ira_cn<8><<<gcn, 384, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
+            else k_ira_cn<kICS><<<gcn, 384, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
         }
         k_ira_out<<<dim3(tiles, b), 256, 0, st>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
                                                   s->n, s->k, s->q);

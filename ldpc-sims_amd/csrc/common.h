@@ -483,6 +483,11 @@ size_t qc_workspace(const QCSpec* s, int64_t B, const ldpc_params& p);
 int qc_decode(const QCSpec* s, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
               int32_t* iters_used, char* ws, hipStream_t st);
 
+// tanh-SP register kernels, two passes (qc.hip k_qc_sp_st, qc_sl_sp.h): one byte per wave / unit in the decode's
+// workspace, written by the plain pass (1 = its LLRs hold an exact zero: left to the a == 1 rule's pass), read by
+// the second.  qc_decode sets it for the launchers it calls on this host thread.
+uint8_t*& qc_sp_flags();
+
 // IRA codes with the DVB-S2 structure (Z = 360), min-sum (ira.hip)
 struct IRASpec;
 IRASpec* ira_detect(int m, int n, const int32_t* row_ptr, const int32_t* col_idx, int device);

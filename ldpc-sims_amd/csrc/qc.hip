@@ -1152,7 +1152,8 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 template <class C, bool EARLY, int PASS = 1>
 __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const float* __restrict__ llr, int64_t B, int iters,
                                                                        float clamp, int flags, uint8_t* __restrict__ bits,
-                                                                       float* __restrict__ soft, int32_t* __restrict__ iters_used) {
+                                                                       float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                                                                       uint8_t* __restrict__ zflags) {
     constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB);
     static_assert(Z <= 64, "register kernel needs Z <= 64");
@@ -1166,6 +1167,10 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
+    const int64_t wu = __builtin_amdgcn_readfirstlane((int)wave);  // this wave's flag (wave-uniform)
+    if constexpr (PASS == 2) {
+        if (wave * CPW >= B || zflags[wu] == 0) return;  // the plain pass decoded this wave
+    }
     // lane rotations through a per-wave LDS row instead of ds_bpermute (see QC_PH_LDSROT)
     constexpr bool LDSROT = EARLY ? QC_SP_LDSROT_EARLY : QC_SP_LDSROT;
     __shared__ float Rw[LDSROT ? 256 : 1];
@@ -1214,9 +1219,10 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     }
     // a wave whose codewords hold an exact-zero LLR runs the loop with the a == 1 rule (PASS 2); every other wave
     // the plain loop (PASS 1; the rule changes nothing there unless an s cancels exactly)
-    if constexpr (PASS != 0) {
+    if constexpr (PASS == 1) {
         const bool zin = __ballot(zl) != 0;
-        if (zin != (PASS == 2)) return;
+        if (lane == 0 && wave * CPW < B) zflags[wu] = zin ? 1 : 0;
+        if (zin) return;  // the a == 1 rule's pass decodes this wave
     }
     float msg[NE];
 #pragma unroll
@@ -1460,10 +1466,11 @@ static int launch_sp_es(const void* llr, int64_t B, const ldpc_params& p, uint8_
     const int tpb = sp_tpb<true>();
     const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
     if constexpr (QC_SP_FIXZ) {
-        k_qc_sp_st<C, true, 1><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used);
-        k_qc_sp_st<C, true, 2><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used);
+        uint8_t* zf = qc_sp_flags();
+        k_qc_sp_st<C, true, 1><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zf);
+        k_qc_sp_st<C, true, 2><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zf);
     } else {
-        k_qc_sp_st<C, true, 0><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used);
+        k_qc_sp_st<C, true, 0><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, nullptr);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "qc kernel launch: %s", hipGetErrorString(e));
@@ -1525,14 +1532,15 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
                 else return qc_launch_ms_es_wifi1296_23(llr, B, p, bits, soft, used, st);
             }
         } else {
-            if (es) k_qc_sp_st<C, true, 0><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+            if (es) k_qc_sp_st<C, true, 0><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, nullptr);
         }
         if (!es) {
             if constexpr (QC_SP_FIXZ) {  // the plain pass, then the a == 1 rule's pass for waves with a zero LLR
-                k_qc_sp_st<C, false, 1><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
-                k_qc_sp_st<C, false, 2><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+                uint8_t* zf = qc_sp_flags();
+                k_qc_sp_st<C, false, 1><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zf);
+                k_qc_sp_st<C, false, 2><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zf);
             } else {
-                k_qc_sp_st<C, false, 0><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used);
+                k_qc_sp_st<C, false, 0><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, nullptr);
             }
         }
     } else if (p.algo == LDPC_ALGO_QMIN_SUM && QC_PACKED != 0) {
@@ -1622,11 +1630,22 @@ bool qc_supports(const QCSpec* s, const ldpc_params& p) {
     return p.algo == LDPC_ALGO_MIN_SUM || p.algo == LDPC_ALGO_QMIN_SUM;
 }
 
-size_t qc_workspace(const QCSpec*, int64_t, const ldpc_params&) { return 0; }
+// tanh-SP: one flag byte per wave / unit of the two-pass kernels (qc_sp_flags); B bytes bound every layout
+size_t qc_workspace(const QCSpec*, int64_t B, const ldpc_params& p) {
+    return (p.algo == LDPC_ALGO_TANH_SP && QC_SP_FIXZ) ? (size_t)((B + 255) & ~(int64_t)255) : 0;
+}
+
+uint8_t*& qc_sp_flags() {
+    static thread_local uint8_t* f = nullptr;
+    return f;
+}
 
 int qc_decode(const QCSpec* s, const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
-              int32_t* used, char*, hipStream_t st) {
-    return s->launch_ms(llr, B, p, bits, soft, used, st);
+              int32_t* used, char* ws, hipStream_t st) {
+    qc_sp_flags() = (uint8_t*)ws;
+    const int rc = s->launch_ms(llr, B, p, bits, soft, used, st);
+    qc_sp_flags() = nullptr;
+    return rc;
 }
 #endif  // QC_TU_ES
 

@@ -95,9 +95,11 @@ constexpr int pk_tpb() { return EARLY ? QC_PK_TPB_EARLY : QC_PK_TPB; }
 // wraps past Z puts two sources of one half on a bank (round 4: SQ_LDS_BANK_CONFLICT 19 % of the kernel's LDS
 // cycles).  Interleaved, a rotation by rho = 2v + f reads, for the half of parity e, the half of parity e ^ f at
 // lane index (u + v + f e) mod Z/2: distinct lanes of one half, so every rotation is conflict-free.  The early-stop
-// ballots are permuted the same way (ilv_rot).  A relabelling of lanes: bitwise the same results.
+// ballots are permuted the same way (ilv_rot).  A relabelling of lanes: bitwise the same results.  Off by default:
+// measured 2 % slower on config [3] (round 5, profiles/r05/ab): the conflicts it removes were not on the critical
+// path, and the interleaved addressing costs VALU in the rotation and epilogue.
 #ifndef QC_PK_ILV
-#define QC_PK_ILV 1
+#define QC_PK_ILV 0
 #endif
 template <int Z>
 constexpr int ilv_u(int l) {  // a lane's index within its half; an idle lane (index >= Z/2) that of the lane it aliases

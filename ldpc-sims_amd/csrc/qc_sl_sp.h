@@ -98,7 +98,8 @@ template <class C, bool EARLY, int PASS = 1>
 __global__ __launch_bounds__(C::S * 64)
 __attribute__((amdgpu_waves_per_eu(EARLY ? QC_SL_SP_WAVES_PER_SIMD_EARLY : QC_SL_SP_WAVES_PER_SIMD)))
 void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
-                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
+                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                uint8_t* __restrict__ zflags) {
     constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB), NT = nz_max<C>(), ROW = 2 * 2 * Z;  // floats per exchanged circulant
     static_assert(S > 1 && Z % S == 0 && ZL <= 32, "sliced kernel: Z = S * ZL, ZL <= 32");
@@ -112,6 +113,9 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     const int64_t cw = (int64_t)blockIdx.x * 2 + h;
     const bool live = l < ZL;                // lane carries a frame position
     const bool valid = live && cw < B;       // ... of a real codeword
+    if constexpr (PASS == 2) {
+        if (zflags[blockIdx.x] == 0) return;  // the plain pass decoded this unit (uniform)
+    }
     // idle lanes (l >= ZL) alias this wave's first position for reads (they never store): an exchange read is
     // served per 32-lane half with bank = (address / 4) mod 32, and aliased to position 0 (round 2) the idle
     // lanes of waves k = 1, 2 read a distinct address on a bank their active lanes use — one extra LDS cycle
@@ -158,7 +162,10 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     // the unit's two codewords hold an exact-zero LLR: the loop with the a == 1 rule (common.h cn_ds_row FIX);
     // the barrier also orders the L rows of LM == 1
     const bool zin = __syncthreads_or(zl);
-    if (PASS != 0 && zin != (PASS == 2)) return;  // uniform over the unit
+    if constexpr (PASS == 1) {
+        if (threadIdx.x == 0) zflags[blockIdx.x] = zin ? 1 : 0;
+        if (zin) return;  // uniform over the unit: the a == 1 rule's pass decodes it
+    }
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
@@ -423,7 +430,8 @@ constexpr int rs_q() {  // the smallest Q with Q * Q >= Z (9 for 81)
 template <class C, int PASS = 1>  // PASS: as k_qc_sp_sl's
 __global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_RS_WAVES_PER_SIMD)))
 void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
-                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
+                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                uint8_t* __restrict__ zflags) {
     constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB), NR = rs_rot_total<C>(), N0 = NE - NR;
     constexpr int Q = rs_q<Z>(), NA = (Z - 1) / Q + 1;
@@ -437,6 +445,9 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
     const int64_t cw = (int64_t)blockIdx.x * 2 + h;
     const bool live = l < ZL;                // lane carries a frame position (stores are live lanes only)
     const bool valid = live && cw < B;
+    if constexpr (PASS == 2) {
+        if (zflags[blockIdx.x] == 0) return;  // the plain pass decoded this unit (uniform)
+    }
     // idle lanes read at their wave's first position (a broadcast, see k_qc_sp_sl) and never store; with
     // QC_RS_IDLE_DUP they shadow lane l - ZL instead — the same loads, so the same values, written to the same
     // slots by the same instruction — and the stores need no exec mask
@@ -509,7 +520,10 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
     // (every check slot zeroed) and: the unit's codewords hold an exact-zero LLR -> the loop with the a == 1
     // rule (common.h cn_ds_row FIX)
     const bool zin = __syncthreads_or(zl);
-    if (PASS != 0 && zin != (PASS == 2)) return;  // uniform over the unit
+    if constexpr (PASS == 1) {
+        if (threadIdx.x == 0) zflags[blockIdx.x] = zin ? 1 : 0;
+        if (zin) return;  // uniform over the unit: the a == 1 rule's pass decodes it
+    }
     const float cmax2 = sp_cmax2(clamp);  // check outputs in log2 units (common.h)
     // column j's messages in ascending row order: (row, slot) of its k-th edge
     auto col_rt = [](int j, int kk) constexpr {

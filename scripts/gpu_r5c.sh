@@ -1,0 +1,13 @@
+# round 5 session c: flag-based second pass (tanh-SP a == 1 rule), QC_PK_ILV off, IRA tasks-per-workgroup sweep
+set -o pipefail
+export TMPDIR=/tmp
+OUT=${OUT:-gpurun_out/r5c}; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py tests/test_gpu_config2.py tests/test_gpu_ira.py -k "packed or qms or quantized or zero or config2 or config3 or resident or kernels_agree or tanh or ira" > $OUT/pytest.log 2>&1; rc=$?; tail -5 $OUT/pytest.log; [ $rc -eq 0 ] || exit 1
+C4="--code dvbs2_12 --iters 50 --batch 4096 --ebn0 0:0.5:2 --steps 5 --warmup 1 --no-cpu-baseline --no-dropin --no-legs"
+for v in 1:200 2:200 4:200 8:200 16:200 4:100 8:100 4:240; do
+  tpw=${v%%:*}; mb=${v#*:}
+  LDPC_IRA_TPW=$tpw LDPC_IRA_BUDGET_MB=$mb timeout -k 10 300 python bench.py $C4 > $OUT/c4_t${tpw}_b$mb.json 2> $OUT/c4_t${tpw}_b$mb.err || { tail -20 $OUT/c4_t${tpw}_b$mb.err; exit 1; }
+  python -c "import json;d=json.load(open('$OUT/c4_t${tpw}_b$mb.json'));r=d['roofline'];print('tpw $tpw budget $mb', round(d['value']), 'cw/s', round(r['launch_ms'],2), 'ms', d['config']['kernel_path'])"
+done
+OUT=$OUT CONFIGS="c2|--code wifi1944_56 --algo tanh --iters 50 --clamp 20 --batch 32768 --mod 16qam-ofdm --ebn0 4:0.5:9 --no-legs --steps 11 --warmup 3;c3|--code wifi1296_23 --algo qminsum --iters 20 --batch 65536 --early-stop --ebn0 0:0.5:5 --no-legs --steps 22 --warmup 3" \
+  VARIANTS="build_variants/c2_fix0.so build_variants/cur.so build_variants/c2_fix0.so build_variants/cur.so" bash scripts/ab_configs.sh || exit 1

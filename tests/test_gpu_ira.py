@@ -108,6 +108,11 @@ def test_equals_generic_kernels_and_chunking(dvbs2, monkeypatch):
             monkeypatch.setenv("LDPC_IRA_BUDGET_MB", budget)
         bits, z, _ = _decode(dec, x, 12, clamp=20.0)
         assert np.array_equal(bits, gb) and _same(z, gz), budget
+    monkeypatch.delenv("LDPC_IRA_BUDGET_MB", raising=False)
+    for tpw in ("2", "7", "200"):  # tasks per workgroup: ragged last group, one group per codeword
+        monkeypatch.setenv("LDPC_IRA_TPW", tpw)
+        bits, z, _ = _decode(dec, x, 12, clamp=20.0)
+        assert np.array_equal(bits, gb) and _same(z, gz), tpw
 
 
 def test_shaped_code_and_host_pointers():

@@ -483,10 +483,14 @@ size_t qc_workspace(const QCSpec* s, int64_t B, const ldpc_params& p);
 int qc_decode(const QCSpec* s, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
               int32_t* iters_used, char* ws, hipStream_t st);
 
-// tanh-SP register kernels, two passes (qc.hip k_qc_sp_st, qc_sl_sp.h): one byte per wave / unit in the decode's
-// workspace, written by the plain pass (1 = its LLRs hold an exact zero: left to the a == 1 rule's pass), read by
-// the second.  qc_decode sets it for the launchers it calls on this host thread.
-uint8_t*& qc_sp_flags();
+// tanh-SP register kernels, two passes (qc.hip k_qc_sp_st, qc_sl_sp.h): the waves / units whose LLRs hold an
+// exact zero, listed by the plain pass in the decode's workspace ([0] = count, then ids), decoded by the a == 1
+// rule's pass, a small grid walking the list.  qc_decode sets the pointer for the launchers it calls on this
+// host thread; qc_sp_zlist_reset zeroes the count (stream-ordered) before a plain pass.
+uint32_t*& qc_sp_zlist();
+int qc_sp_zlist_reset(hipStream_t st);
+constexpr unsigned kSpPass2Blocks = 1280;  // second-pass grid cap: 5 units per CU
+inline unsigned qc_sp_pass2_grid(unsigned blocks) { return blocks < kSpPass2Blocks ? blocks : kSpPass2Blocks; }
 
 // IRA codes with the DVB-S2 structure (Z = 360), min-sum (ira.hip)
 struct IRASpec;

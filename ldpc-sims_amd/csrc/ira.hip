@@ -390,7 +390,12 @@ static int64_t ira_chunk(const IRASpec* s, int64_t B) {
     const int64_t per = 8 * (int64_t)s->n + 12 * (int64_t)s->M;
     int64_t bc = budget / per / 8 * 8;
     if (bc < 8) bc = 8;
-    return bc < B ? bc : B;
+    if (bc >= B) return B;
+    // balanced: the fewest chunks of at most bc codewords, equal sizes (rounded up to 8) — no short last chunk
+    // whose launches would leave most of the chip idle
+    const int64_t nch = (B + bc - 1) / bc;
+    const int64_t eq = ((B + nch - 1) / nch + 7) / 8 * 8;
+    return eq < bc ? eq : bc;
 }
 
 size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {

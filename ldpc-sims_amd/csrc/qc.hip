@@ -1147,13 +1147,14 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 // iters_used = it and its z_it is parked in its own L region of LDS (its lanes keep computing for the
 // wave's other codeword, discarded).  Bitwise equal to the generic path's early stop.
 // PASS (the a == 1 rule, common.h cn_ds_row FIX): 1 = the plain loop for waves without an exact-zero LLR (the
-// others return at once), 2 = the FIX loop for the waves with one (the others return) — two launches, so each
-// kernel keeps its own register allocation; 0 = the plain loop for every wave (QC_SP_FIXZ 0).
-template <class C, bool EARLY, int PASS = 1>
-__global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const float* __restrict__ llr, int64_t B, int iters,
-                                                                       float clamp, int flags, uint8_t* __restrict__ bits,
-                                                                       float* __restrict__ soft, int32_t* __restrict__ iters_used,
-                                                                       uint8_t* __restrict__ zflags) {
+// others append their wave id to `zlist` and return at once), 2 = the FIX loop for the listed waves (a small
+// grid whose waves walk the list) — two launches, so each kernel keeps its own register allocation; 0 = the
+// plain loop for every wave (QC_SP_FIXZ 0).  zlist: [0] = count, [1 ..] = wave ids (qc_sp_zlist).
+template <class C, bool EARLY, int PASS>
+__device__ __forceinline__ void qc_sp_st_wave(int64_t wave_listed, const float* __restrict__ llr, int64_t B, int iters,
+                                              float clamp, int flags, uint8_t* __restrict__ bits,
+                                              float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                                              uint32_t* __restrict__ zlist) {
     constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB);
     static_assert(Z <= 64, "register kernel needs Z <= 64");
@@ -1161,16 +1162,12 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     const int lane = threadIdx.x & 63;
     const int half = (CPW == 2) ? (lane >> 5) : 0;
     const int z = (CPW == 2) ? (lane & 31) : lane;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t wave = PASS == 2 ? wave_listed : ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t cw = wave * CPW + half;
     const bool valid = (z < Z) && (cw < B);
     const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
-    const int64_t wu = __builtin_amdgcn_readfirstlane((int)wave);  // this wave's flag (wave-uniform)
-    if constexpr (PASS == 2) {
-        if (wave * CPW >= B || zflags[wu] == 0) return;  // the plain pass decoded this wave
-    }
     // lane rotations through a per-wave LDS row instead of ds_bpermute (see QC_PH_LDSROT)
     constexpr bool LDSROT = EARLY ? QC_SP_LDSROT_EARLY : QC_SP_LDSROT;
     __shared__ float Rw[LDSROT ? 256 : 1];
@@ -1220,9 +1217,10 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     // a wave whose codewords hold an exact-zero LLR runs the loop with the a == 1 rule (PASS 2); every other wave
     // the plain loop (PASS 1; the rule changes nothing there unless an s cancels exactly)
     if constexpr (PASS == 1) {
-        const bool zin = __ballot(zl) != 0;
-        if (lane == 0 && wave * CPW < B) zflags[wu] = zin ? 1 : 0;
-        if (zin) return;  // the a == 1 rule's pass decodes this wave
+        if (__ballot(zl) != 0) {  // the a == 1 rule's pass decodes this wave
+            if (lane == 0) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)wave;
+            return;
+        }
     }
     float msg[NE];
 #pragma unroll
@@ -1403,7 +1401,8 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
     const int zo = (CPW == 2) ? (tid & 31) : (tid & 63);
-    const int64_t cwo = (((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0);
+    const int64_t wo = PASS == 2 ? wave : (((int64_t)blockIdx.x * blockDim.x + tid) >> 6);
+    const int64_t cwo = wo * CPW + ((CPW == 2) ? ((tid >> 5) & 1) : 0);
     const bool parked = EARLY && CPW == 2 && ((done_groups >> (tid & 63)) & 1ull);
     if (zo < Z && cwo < B) {
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
@@ -1419,6 +1418,22 @@ __global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAV
             if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
         });
         if (zo == 0 && iters_used) iters_used[cwo] = (CPW == 2 && ((tid >> 5) & 1)) ? used_hi : used_lo;
+    }
+}
+
+template <class C, bool EARLY, int PASS = 1>
+__global__ __launch_bounds__(256, EARLY ? QC_SP_WAVES_PER_SIMD_EARLY : QC_SP_WAVES_PER_SIMD) void k_qc_sp_st(const float* __restrict__ llr, int64_t B, int iters,
+                                                                       float clamp, int flags, uint8_t* __restrict__ bits,
+                                                                       float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                                                                       uint32_t* __restrict__ zlist) {
+    if constexpr (PASS == 2) {  // the listed waves, walked by this grid's waves
+        const uint32_t n = zlist[0];
+        const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+        for (uint32_t i = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6); i < n; i += nw)
+            qc_sp_st_wave<C, EARLY, 2>(__builtin_amdgcn_readfirstlane(zlist[1 + i]), llr, B, iters, clamp, flags, bits,
+                                       soft, iters_used, zlist);
+    } else {
+        qc_sp_st_wave<C, EARLY, PASS>(0, llr, B, iters, clamp, flags, bits, soft, iters_used, zlist);
     }
 }
 
@@ -1466,9 +1481,10 @@ static int launch_sp_es(const void* llr, int64_t B, const ldpc_params& p, uint8_
     const int tpb = sp_tpb<true>();
     const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
     if constexpr (QC_SP_FIXZ) {
-        uint8_t* zf = qc_sp_flags();
-        k_qc_sp_st<C, true, 1><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zf);
-        k_qc_sp_st<C, true, 2><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zf);
+        uint32_t* zl = qc_sp_zlist();
+        if (const int rc = qc_sp_zlist_reset(st)) return rc;
+        k_qc_sp_st<C, true, 1><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zl);
+        k_qc_sp_st<C, true, 2><<<qc_sp_pass2_grid(blocks), tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zl);
     } else {
         k_qc_sp_st<C, true, 0><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, nullptr);
     }
@@ -1536,9 +1552,10 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         }
         if (!es) {
             if constexpr (QC_SP_FIXZ) {  // the plain pass, then the a == 1 rule's pass for waves with a zero LLR
-                uint8_t* zf = qc_sp_flags();
-                k_qc_sp_st<C, false, 1><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zf);
-                k_qc_sp_st<C, false, 2><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zf);
+                uint32_t* zl = qc_sp_zlist();
+                if (const int rc = qc_sp_zlist_reset(st)) return rc;
+                k_qc_sp_st<C, false, 1><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zl);
+                k_qc_sp_st<C, false, 2><<<qc_sp_pass2_grid(blocks_sp), tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zl);
             } else {
                 k_qc_sp_st<C, false, 0><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, nullptr);
             }
@@ -1630,21 +1647,26 @@ bool qc_supports(const QCSpec* s, const ldpc_params& p) {
     return p.algo == LDPC_ALGO_MIN_SUM || p.algo == LDPC_ALGO_QMIN_SUM;
 }
 
-// tanh-SP: one flag byte per wave / unit of the two-pass kernels (qc_sp_flags); B bytes bound every layout
+// tanh-SP: the zero-LLR list of the two-pass kernels (qc_sp_zlist): a count and at most one id per codeword
 size_t qc_workspace(const QCSpec*, int64_t B, const ldpc_params& p) {
-    return (p.algo == LDPC_ALGO_TANH_SP && QC_SP_FIXZ) ? (size_t)((B + 255) & ~(int64_t)255) : 0;
+    return (p.algo == LDPC_ALGO_TANH_SP && QC_SP_FIXZ) ? (size_t)((4 * (B + 1) + 255) & ~(int64_t)255) : 0;
 }
 
-uint8_t*& qc_sp_flags() {
-    static thread_local uint8_t* f = nullptr;
+uint32_t*& qc_sp_zlist() {
+    static thread_local uint32_t* f = nullptr;
     return f;
+}
+
+int qc_sp_zlist_reset(hipStream_t st) {
+    if (hipMemsetAsync(qc_sp_zlist(), 0, 4, st) != hipSuccess) return set_error(LDPC_EHIP, "zero-LLR list reset failed");
+    return LDPC_OK;
 }
 
 int qc_decode(const QCSpec* s, const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
               int32_t* used, char* ws, hipStream_t st) {
-    qc_sp_flags() = (uint8_t*)ws;
+    qc_sp_zlist() = (uint32_t*)ws;
     const int rc = s->launch_ms(llr, B, p, bits, soft, used, st);
-    qc_sp_flags() = nullptr;
+    qc_sp_zlist() = nullptr;
     return rc;
 }
 #endif  // QC_TU_ES

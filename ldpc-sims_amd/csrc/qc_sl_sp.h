@@ -92,14 +92,15 @@ __device__ __forceinline__ void sl_barrier() {
     if constexpr (!QC_SL_DIAG_NOBAR) __syncthreads();
 }
 
-// PASS: as k_qc_sp_st's (qc.hip) — 1 = the plain loop for units without an exact-zero LLR, 2 = the a == 1 rule's
-// loop for units with one, 0 = the plain loop for every unit
-template <class C, bool EARLY, int PASS = 1>
-__global__ __launch_bounds__(C::S * 64)
-__attribute__((amdgpu_waves_per_eu(EARLY ? QC_SL_SP_WAVES_PER_SIMD_EARLY : QC_SL_SP_WAVES_PER_SIMD)))
-void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
-                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used,
-                uint8_t* __restrict__ zflags) {
+// PASS: as k_qc_sp_st's (qc.hip) — 1 = the plain loop for units without an exact-zero LLR (the others are
+// listed in zlist), 2 = the a == 1 rule's loop for the listed units, 0 = the plain loop for every unit.  A unit
+// = one workgroup's two codewords; unit_listed is the unit of PASS 2 (the others use the block index).
+template <class C, bool EARLY, int PASS>
+__device__ __forceinline__ void qc_sp_sl_unit(uint32_t unit_listed, const float* __restrict__ llr, int64_t B, int iters,
+                                              float clamp, int flags, uint8_t* __restrict__ bits,
+                                              float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                                              uint32_t* __restrict__ zlist) {
+    const int64_t unit = PASS == 2 ? (int64_t)unit_listed : (int64_t)blockIdx.x;
     constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB), NT = nz_max<C>(), ROW = 2 * 2 * Z;  // floats per exchanged circulant
     static_assert(S > 1 && Z % S == 0 && ZL <= 32, "sliced kernel: Z = S * ZL, ZL <= 32");
@@ -110,12 +111,9 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     __shared__ float Lsh[LM == 1 ? 2 * NB * Z : 1];  // L of both codewords: [half][j][position]
     const int k = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // slot of this wave
     const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
-    const int64_t cw = (int64_t)blockIdx.x * 2 + h;
+    const int64_t cw = unit * 2 + h;
     const bool live = l < ZL;                // lane carries a frame position
     const bool valid = live && cw < B;       // ... of a real codeword
-    if constexpr (PASS == 2) {
-        if (zflags[blockIdx.x] == 0) return;  // the plain pass decoded this unit (uniform)
-    }
     // idle lanes (l >= ZL) alias this wave's first position for reads (they never store): an exchange read is
     // served per 32-lane half with bank = (address / 4) mod 32, and aliased to position 0 (round 2) the idle
     // lanes of waves k = 1, 2 read a distinct address on a bank their active lanes use — one extra LDS cycle
@@ -163,8 +161,10 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     // the barrier also orders the L rows of LM == 1
     const bool zin = __syncthreads_or(zl);
     if constexpr (PASS == 1) {
-        if (threadIdx.x == 0) zflags[blockIdx.x] = zin ? 1 : 0;
-        if (zin) return;  // uniform over the unit: the a == 1 rule's pass decodes it
+        if (zin) {  // uniform over the unit: the a == 1 rule's pass decodes it
+            if (threadIdx.x == 0) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)unit;
+            return;
+        }
     }
     float msg[NE];
 #pragma unroll
@@ -194,7 +194,7 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     __shared__ uint8_t Hb[EARLY ? NB * HROW : 1];
     __shared__ uint32_t Fl[2 * S];
     __shared__ float Zp[EARLY ? 2 * NB * Z : 1];  // parked z of converged codewords, [half][j][position]
-    const int64_t cwp = (int64_t)blockIdx.x * 2;
+    const int64_t cwp = unit * 2;
     bool done0 = cwp >= B, done1 = cwp + 1 >= B;  // a missing codeword counts as converged
     int used0 = iters, used1 = iters;
 
@@ -325,6 +325,24 @@ void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
     if (valid && k == 0 && l == 0 && iters_used) iters_used[cw] = h ? used1 : used0;
 }
 
+template <class C, bool EARLY, int PASS = 1>
+__global__ __launch_bounds__(C::S * 64)
+__attribute__((amdgpu_waves_per_eu(EARLY ? QC_SL_SP_WAVES_PER_SIMD_EARLY : QC_SL_SP_WAVES_PER_SIMD)))
+void k_qc_sp_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
+                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                uint32_t* __restrict__ zlist) {
+    if constexpr (PASS == 2) {  // the listed units, walked by this grid's workgroups
+        const uint32_t n = zlist[0];
+        for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+            qc_sp_sl_unit<C, EARLY, 2>(__builtin_amdgcn_readfirstlane(zlist[1 + i]), llr, B, iters, clamp, flags, bits,
+                                       soft, iters_used, zlist);
+            __syncthreads();  // the unit's last LDS reads before the next unit's writes
+        }
+    } else {
+        qc_sp_sl_unit<C, EARLY, PASS>(0, llr, B, iters, clamp, flags, bits, soft, iters_used, zlist);
+    }
+}
+
 // ---- resident sliced tanh-SP (config [2]: 802.11n (1944,5/6), Z = 81) ------------------------------
 // k_qc_sp_sl above keeps every message in VGPRs and exchanges the rotated circulants' values through an LDS
 // row per block row: three or four barriers per block row (16 per iteration), SQ_WAIT_ANY 0.39.  Here the
@@ -427,11 +445,12 @@ constexpr int rs_q() {  // the smallest Q with Q * Q >= Z (9 for 81)
     return q;
 }
 
-template <class C, int PASS = 1>  // PASS: as k_qc_sp_sl's
-__global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_RS_WAVES_PER_SIMD)))
-void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
-                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used,
-                uint8_t* __restrict__ zflags) {
+template <class C, int PASS>  // PASS, unit_listed: as qc_sp_sl_unit's
+__device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float* __restrict__ llr, int64_t B, int iters,
+                                              float clamp, int flags, uint8_t* __restrict__ bits,
+                                              float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                                              uint32_t* __restrict__ zlist) {
+    const int64_t unit = PASS == 2 ? (int64_t)unit_listed : (int64_t)blockIdx.x;
     constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB), NR = rs_rot_total<C>(), N0 = NE - NR;
     constexpr int Q = rs_q<Z>(), NA = (Z - 1) / Q + 1;
@@ -442,12 +461,9 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
     char* const Xb = reinterpret_cast<char*>(X);
     const int k = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // slot of this wave
     const int lane = threadIdx.x & 63, h = lane >> 5, l = lane & 31;
-    const int64_t cw = (int64_t)blockIdx.x * 2 + h;
+    const int64_t cw = unit * 2 + h;
     const bool live = l < ZL;                // lane carries a frame position (stores are live lanes only)
     const bool valid = live && cw < B;
-    if constexpr (PASS == 2) {
-        if (zflags[blockIdx.x] == 0) return;  // the plain pass decoded this unit (uniform)
-    }
     // idle lanes read at their wave's first position (a broadcast, see k_qc_sp_sl) and never store; with
     // QC_RS_IDLE_DUP they shadow lane l - ZL instead — the same loads, so the same values, written to the same
     // slots by the same instruction — and the stores need no exec mask
@@ -521,8 +537,10 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
     // rule (common.h cn_ds_row FIX)
     const bool zin = __syncthreads_or(zl);
     if constexpr (PASS == 1) {
-        if (threadIdx.x == 0) zflags[blockIdx.x] = zin ? 1 : 0;
-        if (zin) return;  // uniform over the unit: the a == 1 rule's pass decodes it
+        if (zin) {  // uniform over the unit: the a == 1 rule's pass decodes it
+            if (threadIdx.x == 0) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)unit;
+            return;
+        }
     }
     const float cmax2 = sp_cmax2(clamp);  // check outputs in log2 units (common.h)
     // column j's messages in ascending row order: (row, slot) of its k-th edge
@@ -646,7 +664,7 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
     // bits out)
     const int lane_e = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     const int le = lane_e & 31, he = (lane_e >> 5) & 1;
-    const int64_t cwe = (int64_t)blockIdx.x * 2 + he;
+    const int64_t cwe = (PASS == 2 ? unit : (int64_t)blockIdx.x) * 2 + he;
     if (le < ZL && cwe < B) {
         const int zce = pos_of(le);
         static_for<0, NB>([&](auto jj) __attribute__((always_inline)) {
@@ -659,6 +677,23 @@ void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp
             if (soft) soft[o] = (flags & LDPC_F_SOFT_Z) ? zz : 1.0f - 1.0f / (1.0f + Num<float>::exp_(-zz));
         });
         if (k == 0 && le == 0 && iters_used) iters_used[cwe] = iters;
+    }
+}
+
+template <class C, int PASS = 1>
+__global__ __launch_bounds__(C::S * 64) __attribute__((amdgpu_waves_per_eu(QC_RS_WAVES_PER_SIMD)))
+void k_qc_sp_rs(const float* __restrict__ llr, int64_t B, int iters, float clamp, int flags,
+                uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used,
+                uint32_t* __restrict__ zlist) {
+    if constexpr (PASS == 2) {  // the listed units, walked by this grid's workgroups
+        const uint32_t n = zlist[0];
+        for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+            qc_sp_rs_unit<C, 2>(__builtin_amdgcn_readfirstlane(zlist[1 + i]), llr, B, iters, clamp, flags, bits, soft,
+                                iters_used, zlist);
+            __syncthreads();  // the unit's last LDS reads before the next unit's writes
+        }
+    } else {
+        qc_sp_rs_unit<C, PASS>(0, llr, B, iters, clamp, flags, bits, soft, iters_used, zlist);
     }
 }
 

@@ -72,6 +72,22 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
     return out
 
 
+TEST_KERNELS = [(os.path.join(ROOT, "tests", "kern", "cn_rows.hip"), os.path.join(ROOT, "tests", "kern", "libcnrows.so"))]
+
+
+def build_test_kernels(force: bool = False, verbose: bool = False) -> None:
+    """The test-only kernel libraries (tests/kern/*.hip: instantiations of csrc routines the GPU tests check
+    directly), same flags as the product objects."""
+    hdrs = [os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc")) if f.endswith(".h")]
+    for src, out in TEST_KERNELS:
+        if not force and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in [src, *hdrs]):
+            continue
+        cmd = ["hipcc", *FLAGS, "-I", os.path.join(ROOT, "include"), "-I", os.path.join(HERE, "csrc"), "-o", out, src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+
+
 if __name__ == "__main__":
     # python build.py [--force] [--out PATH] [-DNAME=VAL ...]
     args = sys.argv[1:]
@@ -80,3 +96,5 @@ if __name__ == "__main__":
     qcf = next((a.split("=", 1)[1].split() for a in args if a.startswith("--qc-flags=")), None)
     print(build(force="--force" in args or bool(defs) or "--no-per-file" in args or qcf is not None, verbose=True,
                 out=out, defines=defs, per_file="--no-per-file" not in args, qc_flags=qcf))
+    if out == OUT and not defs:
+        build_test_kernels(force="--force" in args, verbose=True)

@@ -382,10 +382,11 @@ bool ira_supports(const IRASpec* s, const ldpc_params& p) {
 }
 
 // codewords per chunk: each chunk's arrays (8n + 12M bytes per codeword) stay in the 256 MiB Infinity Cache for
-// all its iterations; LDPC_IRA_BUDGET_MB overrides (0 = the whole batch in one pass)
+// all its iterations; LDPC_IRA_BUDGET_MB overrides (0 = the whole batch in one pass).  Config [4], B = 4,096
+// (profiles/r05/ab/ab_c4_ira_tpw.txt): 100 MB 28.2k cw/s, 200 MB 32.8k, 240 MB 33.6k, 256 MB 34.0k, 400 MB 25.2k.
 static int64_t ira_chunk(const IRASpec* s, int64_t B) {
     const char* env = getenv("LDPC_IRA_BUDGET_MB");
-    const int64_t budget = (env ? (int64_t)atol(env) : 200) << 20;
+    const int64_t budget = (env ? (int64_t)atol(env) : 256) << 20;
     if (budget <= 0) return B;
     const int64_t per = 8 * (int64_t)s->n + 12 * (int64_t)s->M;
     int64_t bc = budget / per / 8 * 8;
@@ -415,8 +416,11 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     const IRADev t{s->vn, s->vdeg, s->cn, s->cdeg, s->q, s->G, s->k, s->n, s->M};
     const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
     const unsigned tiles = (unsigned)((s->k + 1023) / 1024 + ((kIZ + 63) / 64) * ((s->q + 63) / 64));
-    const char* tenv = getenv("LDPC_IRA_TPW");  // tasks per workgroup (A/B knob)
-    const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 1;
+    // tasks per workgroup: one task is a short wave (a few loads, one store), and at one task per workgroup the
+    // launch is bound by the workgroup dispatch rate (5 resident waves per CU, of 32); 4 tasks: 28.8k -> 33.0k cw/s
+    // (config [4], 200 MB chunks), 16 tasks: 20.8k (too few workgroups)
+    const char* tenv = getenv("LDPC_IRA_TPW");
+    const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 4;
     for (int64_t o = 0; o < B; o += bc) {
         const int b = (int)(B - o < bc ? B - o : bc);
         const int64_t vo = o * s->n;

@@ -483,12 +483,17 @@ size_t qc_workspace(const QCSpec* s, int64_t B, const ldpc_params& p);
 int qc_decode(const QCSpec* s, const void* llr_dev, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
               int32_t* iters_used, char* ws, hipStream_t st);
 
-// tanh-SP register kernels, two passes (qc.hip k_qc_sp_st, qc_sl_sp.h): the waves / units whose LLRs hold an
-// exact zero, listed by the plain pass in the decode's workspace ([0] = count, then ids), decoded by the a == 1
-// rule's pass, a small grid walking the list.  qc_decode sets the pointer for the launchers it calls on this
-// host thread; qc_sp_zlist_reset zeroes the count (stream-ordered) before a plain pass.
+// tanh-SP register kernels, two passes (qc.hip k_qc_sp_st, qc_sl_sp.h): qc_sp_fork zeroes the list, runs
+// k_sp_zero_scan on st (the waves / units whose LLRs hold an exact zero: [0] = count, [1 .. B] ids, then one flag
+// byte per unit, in the decode's workspace) and forks a second stream from it; the a == 1 rule's pass walks the
+// list on that stream while the plain pass (which skips flagged units) runs on st; qc_sp_join joins them.
+// qc_decode sets the workspace pointer for the launchers it calls on this host thread.
 uint32_t*& qc_sp_zlist();
-int qc_sp_zlist_reset(hipStream_t st);
+__host__ __device__ inline uint8_t* qc_sp_zflag(uint32_t* zlist, int64_t B) {
+    return reinterpret_cast<uint8_t*>(zlist + 1 + B);
+}
+int qc_sp_fork(const float* llr, int64_t B, int n, int cpu, hipStream_t st, hipStream_t* s2);
+int qc_sp_join(hipStream_t st);
 constexpr unsigned kSpPass2Blocks = 1280;  // second-pass grid cap: 5 units per CU
 inline unsigned qc_sp_pass2_grid(unsigned blocks) { return blocks < kSpPass2Blocks ? blocks : kSpPass2Blocks; }
 

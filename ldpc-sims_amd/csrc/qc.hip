@@ -1146,10 +1146,11 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 // each check's frame on the scalar unit (as k_qc_ms_st); a codeword whose syndrome is zero stops with
 // iters_used = it and its z_it is parked in its own L region of LDS (its lanes keep computing for the
 // wave's other codeword, discarded).  Bitwise equal to the generic path's early stop.
-// PASS (the a == 1 rule, common.h cn_ds_row FIX): 1 = the plain loop for waves without an exact-zero LLR (the
-// others append their wave id to `zlist` and return at once), 2 = the FIX loop for the listed waves (a small
-// grid whose waves walk the list) — two launches, so each kernel keeps its own register allocation; 0 = the
-// plain loop for every wave (QC_SP_FIXZ 0).  zlist: [0] = count, [1 ..] = wave ids (qc_sp_zlist).
+// PASS (the a == 1 rule, common.h cn_ds_row FIX): k_sp_zero_scan lists the waves whose codewords hold an
+// exact-zero LLR (zlist: [0] = count, [1 ..] = wave ids, then one flag byte per wave — qc_sp_zflag); 1 = the plain
+// loop for the unlisted waves (a listed one returns at once), 2 = the FIX loop for the listed waves (a small grid
+// whose waves walk the list, on a second stream beside PASS 1: qc_sp_fork / qc_sp_join) — two kernels, so each
+// keeps its own register allocation; 0 = the plain loop for every wave (QC_SP_FIXZ 0).
 template <class C, bool EARLY, int PASS>
 __device__ __forceinline__ void qc_sp_st_wave(int64_t wave_listed, const float* __restrict__ llr, int64_t B, int iters,
                                               float clamp, int flags, uint8_t* __restrict__ bits,
@@ -1168,6 +1169,9 @@ __device__ __forceinline__ void qc_sp_st_wave(int64_t wave_listed, const float* 
     const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
     const int base4m = base4 - 4 * Z;
+    if constexpr (PASS == 1) {  // a wave whose codewords hold an exact-zero LLR: the a == 1 rule's pass decodes it
+        if (wave * CPW < B && qc_sp_zflag(zlist, B)[__builtin_amdgcn_readfirstlane((int)wave)]) return;
+    }
     // lane rotations through a per-wave LDS row instead of ds_bpermute (see QC_PH_LDSROT)
     constexpr bool LDSROT = EARLY ? QC_SP_LDSROT_EARLY : QC_SP_LDSROT;
     __shared__ float Rw[LDSROT ? 256 : 1];
@@ -1201,7 +1205,6 @@ __device__ __forceinline__ void qc_sp_st_wave(int64_t wave_listed, const float* 
     __shared__ float Ls[(sp_tpb<EARLY>() / 64) * CPW * N];
     const int lbase = ((threadIdx.x >> 6) * CPW + half) * N + z;
     const int lbase4 = lbase * 4;  // bytes (lds_reload)
-    bool zl = false;  // an exact-zero LLR in this lane's variables (common.h cn_ds_row FIX)
     {
         const int64_t cwbase = valid ? cw * N : 0;
         const float vmask = valid ? 1.0f : 0.0f;
@@ -1210,17 +1213,8 @@ __device__ __forceinline__ void qc_sp_st_wave(int64_t wave_listed, const float* 
             int t = z + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const float x = llr[cwbase + j * Z + (valid ? t : 0)] * vmask;
-            zl |= valid && x == 0.0f;
             if (z < Z) Ls[lbase + j * Z] = -x;  // L = -llr (bp.py:47)
         });
-    }
-    // a wave whose codewords hold an exact-zero LLR runs the loop with the a == 1 rule (PASS 2); every other wave
-    // the plain loop (PASS 1; the rule changes nothing there unless an s cancels exactly)
-    if constexpr (PASS == 1) {
-        if (__ballot(zl) != 0) {  // the a == 1 rule's pass decodes this wave
-            if (lane == 0) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)wave;
-            return;
-        }
     }
     float msg[NE];
 #pragma unroll
@@ -1482,9 +1476,11 @@ static int launch_sp_es(const void* llr, int64_t B, const ldpc_params& p, uint8_
     const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
     if constexpr (QC_SP_FIXZ) {
         uint32_t* zl = qc_sp_zlist();
-        if (const int rc = qc_sp_zlist_reset(st)) return rc;
+        hipStream_t s2;
+        if (const int rc = qc_sp_fork((const float*)llr, B, C::NB * C::Z, CPW, st, &s2)) return rc;
+        k_qc_sp_st<C, true, 2><<<qc_sp_pass2_grid(blocks), tpb, 0, s2>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zl);
         k_qc_sp_st<C, true, 1><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zl);
-        k_qc_sp_st<C, true, 2><<<qc_sp_pass2_grid(blocks), tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, zl);
+        if (const int rc = qc_sp_join(st)) return rc;
     } else {
         k_qc_sp_st<C, true, 0><<<blocks, tpb, 0, st>>>((const float*)llr, B, p.iters, p.clamp, p.flags, bits, (float*)soft, used, nullptr);
     }
@@ -1553,9 +1549,11 @@ static int launch_ms(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
         if (!es) {
             if constexpr (QC_SP_FIXZ) {  // the plain pass, then the a == 1 rule's pass for waves with a zero LLR
                 uint32_t* zl = qc_sp_zlist();
-                if (const int rc = qc_sp_zlist_reset(st)) return rc;
+                hipStream_t s2;
+                if (const int rc = qc_sp_fork(x, B, C::NB * C::Z, CPW, st, &s2)) return rc;
+                k_qc_sp_st<C, false, 2><<<qc_sp_pass2_grid(blocks_sp), tpb_sp, 0, s2>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zl);
                 k_qc_sp_st<C, false, 1><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zl);
-                k_qc_sp_st<C, false, 2><<<qc_sp_pass2_grid(blocks_sp), tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, zl);
+                if (const int rc = qc_sp_join(st)) return rc;
             } else {
                 k_qc_sp_st<C, false, 0><<<blocks_sp, tpb_sp, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, nullptr);
             }
@@ -1647,9 +1645,10 @@ bool qc_supports(const QCSpec* s, const ldpc_params& p) {
     return p.algo == LDPC_ALGO_MIN_SUM || p.algo == LDPC_ALGO_QMIN_SUM;
 }
 
-// tanh-SP: the zero-LLR list of the two-pass kernels (qc_sp_zlist): a count and at most one id per codeword
+// tanh-SP: the zero-LLR list of the two-pass kernels (qc_sp_zlist, qc_sp_zflag): a count, at most one id per
+// codeword, then one flag byte per codeword
 size_t qc_workspace(const QCSpec*, int64_t B, const ldpc_params& p) {
-    return (p.algo == LDPC_ALGO_TANH_SP && QC_SP_FIXZ) ? (size_t)((4 * (B + 1) + 255) & ~(int64_t)255) : 0;
+    return (p.algo == LDPC_ALGO_TANH_SP && QC_SP_FIXZ) ? (size_t)((4 * (B + 1) + B + 255) & ~(int64_t)255) : 0;
 }
 
 uint32_t*& qc_sp_zlist() {
@@ -1657,8 +1656,81 @@ uint32_t*& qc_sp_zlist() {
     return f;
 }
 
-int qc_sp_zlist_reset(hipStream_t st) {
-    if (hipMemsetAsync(qc_sp_zlist(), 0, 4, st) != hipSuccess) return set_error(LDPC_EHIP, "zero-LLR list reset failed");
+// one wave per unit of `cpu` consecutive codewords (n LLRs each, row-major): flag = an exact-zero LLR (+-0) in the
+// unit, listed once.  Reads the batch's LLRs once (B n 4 bytes) so that the a == 1 rule's units can run beside the
+// plain pass instead of after it.
+__global__ __launch_bounds__(256) void k_sp_zero_scan(const float* __restrict__ llr, int64_t B, int n, int cpu,
+                                                      int64_t units, uint32_t* __restrict__ zlist) {
+    const int64_t u = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (u >= units) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const int64_t c0 = u * cpu, c1 = (c0 + cpu < B) ? c0 + cpu : B;
+    const float* p = llr + c0 * n;
+    const int64_t cnt = (c1 - c0) * n;
+    bool z = false;
+    int64_t i0 = 0;
+    if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+        const float4* p4 = reinterpret_cast<const float4*>(p);
+        const int64_t n4 = cnt >> 2;
+        for (int64_t i = lane; i < n4; i += 64) {
+            const float4 v = p4[i];
+            z |= (v.x == 0.0f) | (v.y == 0.0f) | (v.z == 0.0f) | (v.w == 0.0f);
+        }
+        i0 = n4 << 2;
+    }
+    for (int64_t i = i0 + lane; i < cnt; i += 64) z |= p[i] == 0.0f;
+    const bool zu = __ballot(z) != 0;
+    if (lane == 0) {
+        qc_sp_zflag(zlist, B)[u] = zu ? 1 : 0;
+        if (zu) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)u;
+    }
+}
+
+namespace {
+struct SpAux {  // per host thread and device: the second stream and the fork / join events
+    hipStream_t s2 = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+SpAux* sp_aux() {
+    static thread_local SpAux aux[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SpAux& a = aux[dev];
+    if (!a.join) {
+        if (!a.s2 && hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking) != hipSuccess) {
+            a.s2 = nullptr;
+            return nullptr;
+        }
+        if (!a.fork && hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) != hipSuccess) {
+            a.fork = nullptr;
+            return nullptr;
+        }
+        if (hipEventCreateWithFlags(&a.join, hipEventDisableTiming) != hipSuccess) {
+            a.join = nullptr;
+            return nullptr;
+        }
+    }
+    return &a;
+}
+}  // namespace
+
+int qc_sp_fork(const float* llr, int64_t B, int n, int cpu, hipStream_t st, hipStream_t* s2) {
+    uint32_t* zl = qc_sp_zlist();
+    SpAux* a = sp_aux();
+    if (!zl || !a) return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: no workspace or auxiliary stream");
+    if (hipMemsetAsync(zl, 0, 4, st) != hipSuccess) return set_error(LDPC_EHIP, "zero-LLR list reset failed");
+    const int64_t units = (B + cpu - 1) / cpu;
+    k_sp_zero_scan<<<(unsigned)((units + 3) / 4), 256, 0, st>>>(llr, B, n, cpu, units, zl);
+    if (hipEventRecord(a->fork, st) != hipSuccess || hipStreamWaitEvent(a->s2, a->fork, 0) != hipSuccess)
+        return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: stream fork failed");
+    *s2 = a->s2;
+    return LDPC_OK;
+}
+
+int qc_sp_join(hipStream_t st) {
+    SpAux* a = sp_aux();
+    if (!a || hipEventRecord(a->join, a->s2) != hipSuccess || hipStreamWaitEvent(st, a->join, 0) != hipSuccess)
+        return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: stream join failed");
     return LDPC_OK;
 }
 

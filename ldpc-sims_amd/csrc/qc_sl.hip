@@ -181,17 +181,23 @@ static int launch_sl(const void* llr, int64_t B, const ldpc_params& p, uint8_t* 
             static_assert(std::is_same_v<C, Wifi1944_56>, "one sliced code");
             qc_launch_sp_sl_es_wifi1944_56(x, B, p, bits, sf, used, st);
         } else if (QC_SL_SP_RS) {  // the plain pass, then the a == 1 rule's pass for units with a zero LLR
-            if (QC_SP_FIXZ)
-                if (const int rc = qc_sp_zlist_reset(st)) return rc;
+            hipStream_t s2 = st;
+            if (QC_SP_FIXZ) {
+                if (const int rc = qc_sp_fork(x, B, C::NB * C::Z, 2, st, &s2)) return rc;
+                k_qc_sp_rs<C, 2><<<qc_sp_pass2_grid(blocks), tb, 0, s2>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, qc_sp_zlist());
+            }
             k_qc_sp_rs<C, QC_SP_FIXZ ? 1 : 0><<<blocks, tb, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, qc_sp_zlist());
             if (QC_SP_FIXZ)
-                k_qc_sp_rs<C, 2><<<qc_sp_pass2_grid(blocks), tb, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, qc_sp_zlist());
+                if (const int rc = qc_sp_join(st)) return rc;
         } else {
-            if (QC_SP_FIXZ)
-                if (const int rc = qc_sp_zlist_reset(st)) return rc;
+            hipStream_t s2 = st;
+            if (QC_SP_FIXZ) {
+                if (const int rc = qc_sp_fork(x, B, C::NB * C::Z, 2, st, &s2)) return rc;
+                k_qc_sp_sl<C, false, 2><<<qc_sp_pass2_grid(blocks), tb, 0, s2>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, qc_sp_zlist());
+            }
             k_qc_sp_sl<C, false, QC_SP_FIXZ ? 1 : 0><<<blocks, tb, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, qc_sp_zlist());
             if (QC_SP_FIXZ)
-                k_qc_sp_sl<C, false, 2><<<qc_sp_pass2_grid(blocks), tb, 0, st>>>(x, B, p.iters, p.clamp, p.flags, bits, sf, used, qc_sp_zlist());
+                if (const int rc = qc_sp_join(st)) return rc;
         }
     } else if (p.algo == LDPC_ALGO_QMIN_SUM) {
         const float qm = (float)p.qmax, am = (float)p.app_max, b = (float)(int)p.beta, qi = 1.0f / p.qstep;

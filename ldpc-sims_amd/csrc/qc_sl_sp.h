@@ -92,15 +92,18 @@ __device__ __forceinline__ void sl_barrier() {
     if constexpr (!QC_SL_DIAG_NOBAR) __syncthreads();
 }
 
-// PASS: as k_qc_sp_st's (qc.hip) — 1 = the plain loop for units without an exact-zero LLR (the others are
-// listed in zlist), 2 = the a == 1 rule's loop for the listed units, 0 = the plain loop for every unit.  A unit
-// = one workgroup's two codewords; unit_listed is the unit of PASS 2 (the others use the block index).
+// PASS: as k_qc_sp_st's (qc.hip) — 1 = the plain loop for the units k_sp_zero_scan did not list, 2 = the a == 1
+// rule's loop for the listed units, 0 = the plain loop for every unit.  A unit = one workgroup's two codewords;
+// unit_listed is the unit of PASS 2 (the others use the block index).
 template <class C, bool EARLY, int PASS>
 __device__ __forceinline__ void qc_sp_sl_unit(uint32_t unit_listed, const float* __restrict__ llr, int64_t B, int iters,
                                               float clamp, int flags, uint8_t* __restrict__ bits,
                                               float* __restrict__ soft, int32_t* __restrict__ iters_used,
                                               uint32_t* __restrict__ zlist) {
     const int64_t unit = PASS == 2 ? (int64_t)unit_listed : (int64_t)blockIdx.x;
+    if constexpr (PASS == 1) {
+        if (unit * 2 < B && qc_sp_zflag(zlist, B)[unit]) return;  // listed: the a == 1 rule's pass (uniform)
+    }
     constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB), NT = nz_max<C>(), ROW = 2 * 2 * Z;  // floats per exchanged circulant
     static_assert(S > 1 && Z % S == 0 && ZL <= 32, "sliced kernel: Z = S * ZL, ZL <= 32");
@@ -125,7 +128,6 @@ __device__ __forceinline__ void qc_sp_sl_unit(uint32_t unit_listed, const float*
     const float* const lp = llr + (valid ? cw * N : 0);
     const int lb = h * NB * Z + zc;
     float Lr[LM == 0 ? NB : 1];
-    bool zl = false;  // an exact-zero LLR among this lane's variables
     auto Lr_at = [&](int j) __attribute__((always_inline)) {
         if constexpr (LM == 2) {
             int z = zc;
@@ -147,25 +149,14 @@ __device__ __forceinline__ void qc_sp_sl_unit(uint32_t unit_listed, const float*
             int t = zc + C::PHI[j];
             t -= (t >= Z) ? Z : 0;
             const float x = valid ? -lp[j * Z + t] : 0.0f;
-            zl |= valid && x == 0.0f;
             if constexpr (LM == 1) {
                 if (live) Lsh[lb + j * Z] = x;
             } else {
                 Lr[j] = x;
             }
         });
-    } else {
-        static_for<0, NB>([&](auto jj) __attribute__((always_inline)) { zl |= valid && Lr_at(decltype(jj)::value) == 0.0f; });
     }
-    // the unit's two codewords hold an exact-zero LLR: the loop with the a == 1 rule (common.h cn_ds_row FIX);
-    // the barrier also orders the L rows of LM == 1
-    const bool zin = __syncthreads_or(zl);
-    if constexpr (PASS == 1) {
-        if (zin) {  // uniform over the unit: the a == 1 rule's pass decodes it
-            if (threadIdx.x == 0) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)unit;
-            return;
-        }
-    }
+    __syncthreads();  // the L rows of LM == 1
     float msg[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) msg[e] = 0.0f;
@@ -451,6 +442,9 @@ __device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float*
                                               float* __restrict__ soft, int32_t* __restrict__ iters_used,
                                               uint32_t* __restrict__ zlist) {
     const int64_t unit = PASS == 2 ? (int64_t)unit_listed : (int64_t)blockIdx.x;
+    if constexpr (PASS == 1) {
+        if (unit * 2 < B && qc_sp_zflag(zlist, B)[unit]) return;  // listed: the a == 1 rule's pass (uniform)
+    }
     constexpr int Z = C::Z, S = C::S, ZL = Z / S, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB), NR = rs_rot_total<C>(), N0 = NE - NR;
     constexpr int Q = rs_q<Z>(), NA = (Z - 1) / Q + 1;
@@ -508,16 +502,9 @@ __device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float*
         t -= (t >= Z) ? Z : 0;
         return lval ? -lp[j * Z + t] : 0.0f;
     };
-    bool zl = false;  // an exact-zero LLR among this lane's variables
     if constexpr (QC_RS_L == 0) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            Lreg[j] = Lload(j, false);
-            zl |= valid && Lreg[j] == 0.0f;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < NB; ++j) zl |= valid && Lload(j, false) == 0.0f;
+        for (int j = 0; j < NB; ++j) Lreg[j] = Lload(j, false);
     }
     auto Lr_at = [&](int j) __attribute__((always_inline)) {
         if constexpr (QC_RS_L == 0) return Lreg[j];
@@ -533,15 +520,7 @@ __device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float*
             });
         });
     }
-    // (every check slot zeroed) and: the unit's codewords hold an exact-zero LLR -> the loop with the a == 1
-    // rule (common.h cn_ds_row FIX)
-    const bool zin = __syncthreads_or(zl);
-    if constexpr (PASS == 1) {
-        if (zin) {  // uniform over the unit: the a == 1 rule's pass decodes it
-            if (threadIdx.x == 0) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)unit;
-            return;
-        }
-    }
+    __syncthreads();  // every check slot zeroed
     const float cmax2 = sp_cmax2(clamp);  // check outputs in log2 units (common.h)
     // column j's messages in ascending row order: (row, slot) of its k-th edge
     auto col_rt = [](int j, int kk) constexpr {

@@ -460,36 +460,21 @@ size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {
     return 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8) + a256((size_t)bc * s->M * 4);
 }
 
-// positions per lane (A/B knob LDPC_IRA_PPL: 1, 2, 3 or 6)
-template <int PPL>
-static void ira_vn_ppl(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* L, float* app,
-                       const float2* S, const uint32_t* MT, int b, int tpw) {
-    if (s->maxdv <= 8) k_ira_vn<8, PPL><<<g, ira_threads<PPL>(), 0, st>>>(t, L, app, S, MT, b, tpw);
-    else k_ira_vn<16, PPL><<<g, ira_threads<PPL>(), 0, st>>>(t, L, app, S, MT, b, tpw);
+// positions per lane: IRA_PPL (compile-time; A/B on config [4], profiles/r05/ab/ab_c4_ira_ppl.txt: 1 fastest)
+#ifndef IRA_PPL
+#define IRA_PPL 1
+#endif
+static void ira_launch_vn(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* L, float* app,
+                          const float2* S, const uint32_t* MT, int b, int tpw) {
+    constexpr int NT = ira_threads<IRA_PPL>();
+    if (s->maxdv <= 8) k_ira_vn<8, IRA_PPL><<<g, NT, 0, st>>>(t, L, app, S, MT, b, tpw);
+    else k_ira_vn<16, IRA_PPL><<<g, NT, 0, st>>>(t, L, app, S, MT, b, tpw);
 }
-template <int PPL>
-static void ira_cn_ppl(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* app, float2* S,
-                       uint32_t* MT, int b, const ldpc_params& p, int tpw) {
-    if (s->maxr <= 8) k_ira_cn<8, PPL><<<g, ira_threads<PPL>(), 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
-    else k_ira_cn<kICS, PPL><<<g, ira_threads<PPL>(), 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
-}
-static void ira_launch_vn(const IRASpec* s, int ppl, unsigned g, hipStream_t st, const IRADev& t, const float* L,
-                          float* app, const float2* S, const uint32_t* MT, int b, int tpw) {
-    switch (ppl) {
-        case 1: ira_vn_ppl<1>(s, g, st, t, L, app, S, MT, b, tpw); break;
-        case 2: ira_vn_ppl<2>(s, g, st, t, L, app, S, MT, b, tpw); break;
-        case 3: ira_vn_ppl<3>(s, g, st, t, L, app, S, MT, b, tpw); break;
-        default: ira_vn_ppl<6>(s, g, st, t, L, app, S, MT, b, tpw);
-    }
-}
-static void ira_launch_cn(const IRASpec* s, int ppl, unsigned g, hipStream_t st, const IRADev& t, const float* app,
-                          float2* S, uint32_t* MT, int b, const ldpc_params& p, int tpw) {
-    switch (ppl) {
-        case 1: ira_cn_ppl<1>(s, g, st, t, app, S, MT, b, p, tpw); break;
-        case 2: ira_cn_ppl<2>(s, g, st, t, app, S, MT, b, p, tpw); break;
-        case 3: ira_cn_ppl<3>(s, g, st, t, app, S, MT, b, p, tpw); break;
-        default: ira_cn_ppl<6>(s, g, st, t, app, S, MT, b, p, tpw);
-    }
+static void ira_launch_cn(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* app, float2* S,
+                          uint32_t* MT, int b, const ldpc_params& p, int tpw) {
+    constexpr int NT = ira_threads<IRA_PPL>();
+    if (s->maxr <= 8) k_ira_cn<8, IRA_PPL><<<g, NT, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
+    else k_ira_cn<kICS, IRA_PPL><<<g, NT, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
 }
 
 int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params& p, uint8_t* bits, float* soft,
@@ -508,8 +493,6 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     // (config [4], 200 MB chunks), 16 tasks: 20.8k (too few workgroups)
     const char* tenv = getenv("LDPC_IRA_TPW");
     const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 4;
-    const char* penv = getenv("LDPC_IRA_PPL");
-    const int ppl = penv && atoi(penv) > 0 ? atoi(penv) : 1;
     for (int64_t o = 0; o < B; o += bc) {
         const int b = (int)(B - o < bc ? B - o : bc);
         const int64_t vo = o * s->n;
@@ -520,9 +503,9 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
             return set_error(LDPC_EHIP, "IRA state init failed");
         const unsigned gvn = cw8 * (unsigned)((s->G + s->q + tpw - 1) / tpw), gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
         for (int it = 0; it <= p.iters; ++it) {
-            ira_launch_vn(s, ppl, gvn, st, t, L, app, S, MT, b, tpw);
+            ira_launch_vn(s, gvn, st, t, L, app, S, MT, b, tpw);
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
-            ira_launch_cn(s, ppl, gcn, st, t, app, S, MT, b, p, tpw);
+            ira_launch_cn(s, gcn, st, t, app, S, MT, b, p, tpw);
         }
         k_ira_out<<<dim3(tiles, b), 256, 0, st>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
                                                   s->n, s->k, s->q);

@@ -69,9 +69,10 @@ def _tail(rows, last):
     return [v for _, v in rows[-last:]] if last else [v for _, v in rows]
 
 
-def summarise(vals, durs, kernel=None, decode_kernels=None, last=0):
+def summarise(vals, durs, kernel=None, decode_kernels=None, last=0, chunks=1):
     """Per-decode counters and duration over the last ``last`` decodes of each pass (0: all), averaged over
-    the passes that collected the counter.  Returns (label, counters, kstats)."""
+    the passes that collected the counter.  ``chunks``: dispatches of the first decode kernel per decode (the
+    IRA path launches its load kernel once per Infinity-Cache chunk).  Returns (label, counters, kstats)."""
     if kernel:
         names = {k for (k, _) in vals if kernel in k}
         if not names:
@@ -91,6 +92,9 @@ def summarise(vals, durs, kernel=None, decode_kernels=None, last=0):
         ids = sorted(i for k, rows in rows_by_kernel.items() if pats[0] in k for i, _ in rows)
         if not ids:
             raise SystemExit(f"no kernel matching {pats[0]}")
+        if len(ids) % chunks:
+            raise SystemExit(f"{len(ids)} dispatches of {pats[0]} are not whole decodes of {chunks} chunks")
+        ids = ids[::chunks]  # the first chunk's dispatch starts a decode
         start, n_dec = (ids[-last], min(last, len(ids))) if last else (ids[0], len(ids))
         tot = sum(v for k, rows in rows_by_kernel.items() if any(p in k for p in pats) for i, v in rows if i >= start)
         return tot / n_dec, start, n_dec
@@ -117,6 +121,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--name", required=True)
     ap.add_argument("--kernel")
+    ap.add_argument("--chunks", type=int, default=1, help="first-decode-kernel dispatches per decode")
     ap.add_argument("--decode-kernels")
     ap.add_argument("--max-clock-ghz", type=float, default=MAX_CLOCK_GHZ)
     ap.add_argument("--last", type=int, default=0, help="use the last N decodes of each pass (the timed loop)")
@@ -126,7 +131,7 @@ def main():
     bench = json.load(open(os.path.join(a.dir, "bench.json")))
     vals = per_kernel(a.dir)
     durs = trace_durations(os.path.join(a.dir, "ks"))
-    label, c, ks = summarise(vals, durs, a.kernel, a.decode_kernels, a.last)
+    label, c, ks = summarise(vals, durs, a.kernel, a.decode_kernels, a.last, a.chunks)
     cfg = bench["config"]
     rec = {"name": a.name, "kernel": label,
            "config": {k: cfg.get(k) for k in ("code", "algo", "iters", "early_stop", "batch_per_gpu", "mod", "kernel_path",

@@ -9,7 +9,7 @@
 # loop's P launches (`--last P`), so the means cover the sweep evenly (the early-stop kernels' work depends
 # on the point), after the clock ramp, and the trace and counters see the same launches.
 #     NAME=headline KERNEL=k_qc_ms ARGS="" bash scripts/gpu_profile.sh
-#     NAME=c4 DKERNELS=k_load_llr,k_vn_,k_cn_,k_final ARGS="--code dvbs2_12 --batch 4096 --ebn0 0:0.5:2" bash ...
+#     NAME=c4 DKERNELS=k_ira_load,k_ira_vn,k_ira_cn,k_ira_out CHUNKS=15 ARGS="--code dvbs2_12 --batch 4096 --ebn0 0:0.5:2" bash ...
 set -o pipefail
 OUT=${OUT:-gpurun_out}; mkdir -p $OUT; export TMPDIR=/tmp
 NAME=${NAME:-headline}
@@ -17,7 +17,7 @@ ARGS="${ARGS:-} --no-dropin --no-legs"  # side measurements and the other config
 GRID=$(python3 -c "import sys; a=sys.argv[1:]; print(a[a.index('--ebn0')+1] if '--ebn0' in a else '0:0.5:5')" $ARGS)
 P=$(python3 -c "import numpy as np,sys; lo,s,hi=map(float,sys.argv[1].split(':')); print(len(np.arange(lo,hi+1e-9,s)))" $GRID)
 PARGS="--steps $P --warmup $P --no-cpu-baseline"
-if [ -n "$DKERNELS" ]; then SEL="--decode-kernels $DKERNELS"; else SEL="--kernel ${KERNEL:-k_qc_ms}"; fi
+if [ -n "$DKERNELS" ]; then SEL="--decode-kernels $DKERNELS --chunks ${CHUNKS:-1}"; else SEL="--kernel ${KERNEL:-k_qc_ms}"; fi
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
 P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE"
 D=$OUT/prof_$NAME

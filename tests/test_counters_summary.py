@@ -66,3 +66,38 @@ def test_rejects_counts_from_other_launches(tmp_path):
     out = subprocess.run([sys.executable, SUMMARY, str(d), "--name", "fake", "--kernel", "k_test", "--last", "3"],
                          capture_output=True, text=True)
     assert out.returncode != 0 and "REJECTED" in (out.stderr + out.stdout)
+
+
+def test_chunked_decodes(tmp_path):
+    """--chunks K: a decode whose first kernel is launched once per chunk (the IRA path) is K dispatches of it;
+    the per-decode sums and the decode count follow, and a count that is not whole decodes is refused."""
+    d = tmp_path / "prof_chunks"
+    (d / "ks").mkdir(parents=True)
+    (d / "pmc1").mkdir()
+    json.dump({"config": {"code": "x"}, "value": 1.0, "ms_per_step": 1.0, "roofline": {"launch_ms": 0.3}},
+              open(d / "bench.json", "w"))
+    rows, i = [], 0
+    for dec in range(4):                       # 4 decodes x 3 chunks x (load, vn) dispatches
+        for ch in range(3):
+            for k in ("k_load(int)", "k_vn(int)"):
+                rows.append((k, i))
+                i += 1
+    with open(d / "ks" / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Dispatch_Id", "Start_Timestamp", "End_Timestamp"])
+        for k, j in rows:
+            w.writerow([k, j, 0, 50_000])           # 0.05 ms each: 0.3 ms per decode
+    with open(d / "pmc1" / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Dispatch_Id", "Counter_Name", "Counter_Value"])
+        for k, j in rows:
+            w.writerow([k, j, "GRBM_GUI_ACTIVE", 8 * 1.0e5])   # 1e5 cycles per dispatch per XCD: 2 GHz
+            w.writerow([k, j, "SQ_INSTS_VALU", 10.0])
+    args = [sys.executable, SUMMARY, str(d), "--name", "c", "--decode-kernels", "k_load,k_vn", "--last", "2"]
+    out = subprocess.run(args + ["--chunks", "3"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout)
+    assert r["kernel_stats"]["calls"] == 2 and abs(r["kernel_stats"]["mean_ms"] - 0.3) < 1e-9
+    assert abs(r["counters_per_launch"]["SQ_INSTS_VALU"] - 60.0) < 1e-9 and abs(r["derived"]["clock_ghz"] - 2.0) < 1e-9
+    bad = subprocess.run(args + ["--chunks", "5"], capture_output=True, text=True)
+    assert bad.returncode != 0 and "whole decodes" in (bad.stderr + bad.stdout)

@@ -84,69 +84,61 @@ __device__ __forceinline__ void rotate_left(float (&c)[D], int rho) {
     });
 }
 
-// Lanes per task: a task's 360 positions over NT = 64 ceil(360 / PPL / 64) threads, PPL positions per lane
-// (pos = lane + q NT).  Every load of a lane's PPL positions is issued before the first is used: PPL times the
-// loads in flight per wave (the kernels wait on memory latency, not on issue).
-template <int PPL>
-constexpr int ira_threads() {
-    return 64 * ((kIZ + PPL * 64 - 1) / (PPL * 64));
+// Workgroup shape: TPP tasks side by side (kIraLanes threads each: 6 waves over the 360 positions, lanes past 360
+// repeat the last position and store nothing), each sub-group running `tpw` tasks one after the other.  Every load
+// of a task is issued before the first is used (a task waits on one memory round trip, not D).
+constexpr int kIraLanes = 384;
+
+template <int TPP>
+__device__ __forceinline__ int ira_pos() {
+    return TPP == 1 ? (int)threadIdx.x : (int)threadIdx.x % kIraLanes;
+}
+template <int TPP>
+__device__ __forceinline__ int ira_sub() {  // wave-uniform: kIraLanes is a multiple of 64
+    return TPP == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / kIraLanes);
 }
 
-// app of PPL information variables (g, pos_q) of degree D: L + their c2v in ascending check order
-template <int D, int PPL>
-__device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int64_t vo, int64_t so,
+// app of information variable (g, pos) of degree D: L + its c2v in ascending check order
+template <int D>
+__device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int64_t vo, int64_t so, int pos,
                                             const float* __restrict__ L, const float2* __restrict__ S,
                                             const uint32_t* __restrict__ MT, float* __restrict__ app) {
-    constexpr int NT = ira_threads<PPL>();
-    float a[PPL], c[PPL][D];
-    int wrapped[PPL];
-#pragma unroll
-    for (int q = 0; q < PPL; ++q) {
-        const int pos = min((int)threadIdx.x + q * NT, kIZ - 1);  // lanes past 360 repeat the last position
-        a[q] = L[vo + pos];
-        wrapped[q] = 0;
-    }
+    const int p = min(pos, kIZ - 1);
+    const float a = L[vo + p];
+    float c[D];
+    int wrapped = 0;
     static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
         constexpr int t = decltype(TT)::value;
         const int e = row[t];  // wave-uniform: a scalar load
         const int ra = e & 0xff, sh = (e >> 8) & 0x1ff, slot = e >> 17;
-#pragma unroll
-        for (int q = 0; q < PPL; ++q) {
-            const int pos = min((int)threadIdx.x + q * NT, kIZ - 1);
-            int b = pos + sh;
-            const bool w = b >= kIZ;
-            b -= w ? kIZ : 0;
-            wrapped[q] += w;
-            const int64_t i = so + (int64_t)ra * kIZ + b;
-            c[q][t] = ira_c2v(S[i], MT[i], slot);
-        }
+        int b = p + sh;
+        const bool w = b >= kIZ;
+        b -= w ? kIZ : 0;
+        wrapped += w;
+        const int64_t i = so + (int64_t)ra * kIZ + b;
+        c[t] = ira_c2v(S[i], MT[i], slot);
     });
+    // entries are sorted by x = a + q s, i.e. by s: the wrapped ones are the last `wrapped` entries and their
+    // checks come first in ascending order
+    const int rho = wrapped == 0 ? 0 : D - wrapped;
+    rotate_left<D>(c, rho);
+    float sum = a;
 #pragma unroll
-    for (int q = 0; q < PPL; ++q) {
-        // entries are sorted by x = a + q s, i.e. by s: the wrapped ones are the last `wrapped` entries and their
-        // checks come first in ascending order
-        const int rho = wrapped[q] == 0 ? 0 : D - wrapped[q];
-        rotate_left<D>(c[q], rho);
-        float s = a[q];
-#pragma unroll
-        for (int t = 0; t < D; ++t) s = s + c[q][t];
-        const int pos = (int)threadIdx.x + q * NT;
-        if (pos < kIZ) app[vo + pos] = s;
-    }
+    for (int t = 0; t < D; ++t) sum = sum + c[t];
+    if (pos < kIZ) app[vo + pos] = sum;
 }
 
 // One task = one variable group (information group g < G, or parity row a = g - G) of one codeword; lanes =
-// the 360 positions (PPL per lane).  Writes app in the permuted layout (information: g*360 + m, parity:
-// k + a*360 + b).  A workgroup runs `tpw` consecutive tasks of its codeword (fewer, longer-lived workgroups).
-template <int MAXDV, int PPL>
-__global__ __launch_bounds__(ira_threads<PPL>()) void k_ira_vn(IRADev t, const float* __restrict__ L,
-                                                               float* __restrict__ app, const float2* __restrict__ S,
-                                                               const uint32_t* __restrict__ MT, int Bc, int tpw) {
-    constexpr int NT = ira_threads<PPL>();
-    const int T = t.G + t.q;
+// the 360 positions.  Writes app in the permuted layout (information: g*360 + m, parity: k + a*360 + b).
+template <int MAXDV, int TPP>
+__global__ __launch_bounds__(kIraLanes * TPP) void k_ira_vn(IRADev t, const float* __restrict__ L,
+                                                             float* __restrict__ app, const float2* __restrict__ S,
+                                                             const uint32_t* __restrict__ MT, int Bc, int tpw) {
+    const int T = t.G + t.q, per = tpw * TPP;
     int cw, tb;
-    if (!ira_task((T + tpw - 1) / tpw, Bc, cw, tb)) return;
-    for (int gi = tb * tpw; gi < T && gi < (tb + 1) * tpw; ++gi) {
+    if (!ira_task((T + per - 1) / per, Bc, cw, tb)) return;
+    const int pos = ira_pos<TPP>();
+    for (int gi = tb * per + ira_sub<TPP>(); gi < T && gi < (tb + 1) * per; gi += TPP) {
         const int64_t vo = (int64_t)cw * t.n + (int64_t)gi * kIZ;
         const int64_t so = (int64_t)cw * t.M;
         if (gi < t.G) {
@@ -154,122 +146,100 @@ __global__ __launch_bounds__(ira_threads<PPL>()) void k_ira_vn(IRADev t, const f
             const int32_t* row = t.vn + gi * kIVS;
             static_for<1, MAXDV + 1>([&](auto DD) __attribute__((always_inline)) {
                 constexpr int D = decltype(DD)::value;
-                if (d == D) ira_vn_info<D, PPL>(row, vo, so, L, S, MT, app);
+                if (d == D) ira_vn_info<D>(row, vo, so, pos, L, S, MT, app);
             });
         } else {
             // parity p_j, j = r + q pos: checks j (its own (r, pos), slot kIPS) and j + 1 (slot kIPS + 1 there)
             const int r = gi - t.G;
-            float a[PPL], c0[PPL], c1[PPL];
-#pragma unroll
-            for (int q = 0; q < PPL; ++q) {
-                const int pos = min((int)threadIdx.x + q * NT, kIZ - 1);
-                a[q] = L[vo + pos];
-                const int64_t i0 = so + (int64_t)r * kIZ + pos;
-                c0[q] = ira_c2v(S[i0], MT[i0], kIPS);
-                int r1 = r + 1, p1 = pos;
-                if (r1 == t.q) {
-                    r1 = 0;
-                    p1 = pos + 1;
-                }
-                const bool has1 = p1 < kIZ;  // j + 1 < M
-                const int64_t i1 = so + (int64_t)r1 * kIZ + (has1 ? p1 : 0);
-                const float x1 = ira_c2v(S[i1], MT[i1], kIPS + 1);
-                c1[q] = has1 ? x1 : -0.0f;  // x + (-0) == x bit for bit: the last parity has one check
+            const int p = min(pos, kIZ - 1);
+            const float a = L[vo + p];
+            const int64_t i0 = so + (int64_t)r * kIZ + p;
+            int r1 = r + 1, p1 = p;
+            if (r1 == t.q) {
+                r1 = 0;
+                p1 = p + 1;
             }
-#pragma unroll
-            for (int q = 0; q < PPL; ++q) {
-                const int pos = (int)threadIdx.x + q * NT;
-                if (pos < kIZ) app[vo + pos] = (a[q] + c0[q]) + c1[q];
-            }
+            const bool has1 = p1 < kIZ;  // j + 1 < M
+            const int64_t i1 = so + (int64_t)r1 * kIZ + (has1 ? p1 : 0);
+            const float c0 = ira_c2v(S[i0], MT[i0], kIPS);
+            const float x1 = ira_c2v(S[i1], MT[i1], kIPS + 1);
+            const float c1 = has1 ? x1 : -0.0f;  // x + (-0) == x bit for bit: the last parity has one check
+            if (pos < kIZ) app[vo + pos] = (a + c0) + c1;
         }
     }
 }
 
-// One task = one check row a of one codeword; lanes = positions b (PPL per lane).  Reads the posteriors of the
-// row's variables and its own state, writes the new state (the oracle's k_cn_ms arithmetic on v2c = app - c2v).
-template <int MAXR, int PPL>
-__global__ __launch_bounds__(ira_threads<PPL>()) void k_ira_cn(IRADev t, const float* __restrict__ app,
-                                                               float2* __restrict__ S, uint32_t* __restrict__ MT,
-                                                               int Bc, float clamp, float alpha, float beta, int tpw) {
-    constexpr int NT = ira_threads<PPL>();
+// One task = one check row a of one codeword; lanes = positions b.  Reads the posteriors of the row's variables
+// and its own state, writes the new state (the oracle's k_cn_ms arithmetic on v2c = app - c2v).
+template <int MAXR, int TPP>
+__global__ __launch_bounds__(kIraLanes * TPP) void k_ira_cn(IRADev t, const float* __restrict__ app,
+                                                             float2* __restrict__ S, uint32_t* __restrict__ MT,
+                                                             int Bc, float clamp, float alpha, float beta, int tpw) {
+    const int per = tpw * TPP;
     int cw, tb;
-    if (!ira_task((t.q + tpw - 1) / tpw, Bc, cw, tb)) return;
-    for (int ra = tb * tpw; ra < t.q && ra < (tb + 1) * tpw; ++ra) {
+    if (!ira_task((t.q + per - 1) / per, Bc, cw, tb)) return;
+    const int pos = ira_pos<TPP>();
+    const int p = min(pos, kIZ - 1);
+    for (int ra = tb * per + ira_sub<TPP>(); ra < t.q && ra < (tb + 1) * per; ra += TPP) {
         const int64_t ao = (int64_t)cw * t.n;
-        const int64_t so = (int64_t)cw * t.M + (int64_t)ra * kIZ;
+        const int64_t si = (int64_t)cw * t.M + (int64_t)ra * kIZ + p;
         const int R = t.cdeg[ra];
         const int32_t* row = t.cn + ra * kICS;
-        float2 st[PPL];
-        uint32_t mt[PPL];
-        float v[PPL][MAXR], ap0[PPL], ap1[PPL];
-#pragma unroll
-        for (int q = 0; q < PPL; ++q) {
-            const int pos = min((int)threadIdx.x + q * NT, kIZ - 1);
-            st[q] = S[so + pos];
-            mt[q] = MT[so + pos];
-            ap0[q] = app[ao + t.k + (int64_t)ra * kIZ + pos];
-            const int64_t pi = ra > 0 ? ao + t.k + (int64_t)(ra - 1) * kIZ + pos
-                                      : ao + t.k + (int64_t)(t.q - 1) * kIZ + (pos > 0 ? pos - 1 : 0);
-            ap1[q] = app[pi];
-        }
+        const float2 st = S[si];
+        const uint32_t mt = MT[si];
+        const float ap0 = app[ao + t.k + (int64_t)ra * kIZ + p];
+        const int64_t pi = ra > 0 ? ao + t.k + (int64_t)(ra - 1) * kIZ + p
+                                  : ao + t.k + (int64_t)(t.q - 1) * kIZ + (p > 0 ? p - 1 : 0);
+        const float ap1 = app[pi];
+        float v[MAXR];
         static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
             constexpr int s = decltype(SS)::value;
             if (s < R) {
                 const int e = row[s];
                 const int g = e & 0xff, sh = e >> 8;
-#pragma unroll
-                for (int q = 0; q < PPL; ++q) {
-                    const int pos = min((int)threadIdx.x + q * NT, kIZ - 1);
-                    int m = pos - sh;
-                    m += m < 0 ? kIZ : 0;
-                    v[q][s] = app[ao + (int64_t)g * kIZ + m];
-                }
+                int m = p - sh;
+                m += m < 0 ? kIZ : 0;
+                v[s] = app[ao + (int64_t)g * kIZ + m];
             }
         });
-#pragma unroll
-        for (int q = 0; q < PPL; ++q) {
-            const int pos = (int)threadIdx.x + q * NT;
-            const float2 sq = st[q];
-            const uint32_t mq = mt[q];
-            float min1 = __builtin_inff(), min2 = __builtin_inff();
-            int idx = -1;
-            uint32_t sgn = 0;
-            auto take = [&](float x, int s) __attribute__((always_inline)) {
-                const float m = fabsf(x);
-                sgn ^= f2u(x);
-                if (m < min1) {
-                    min2 = min1;
-                    min1 = m;
-                    idx = s;
-                } else if (m < min2) {
-                    min2 = m;
-                }
-            };
-            static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
-                constexpr int s = decltype(SS)::value;
-                if (s < R) {
-                    v[q][s] = v[q][s] - ira_c2v(sq, mq, s);
-                    take(v[q][s], s);
-                }
-            });
-            const float vp0 = ap0[q] - ira_c2v(sq, mq, kIPS);
-            const float vp1 = ap1[q] - ira_c2v(sq, mq, kIPS + 1);
-            const bool has_prev = ra > 0 || pos > 0;  // check 0 has no p_{-1}
-            take(vp0, kIPS);
-            if (has_prev) take(vp1, kIPS + 1);
-            const float mag1 = ms_mag(min1, alpha, beta, clamp);
-            const float mag2 = ms_mag(min2, alpha, beta, clamp);
-            uint32_t meta = (uint32_t)idx << 27;
-            static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
-                constexpr int s = decltype(SS)::value;
-                if (s < R) meta |= ((sgn ^ f2u(v[q][s])) >> 31) << s;
-            });
-            meta |= ((sgn ^ f2u(vp0)) >> 31) << kIPS;
-            if (has_prev) meta |= ((sgn ^ f2u(vp1)) >> 31) << (kIPS + 1);
-            if (pos < kIZ) {
-                S[so + pos] = make_float2(mag1, mag2);
-                MT[so + pos] = meta;
+        float min1 = __builtin_inff(), min2 = __builtin_inff();
+        int idx = -1;
+        uint32_t sgn = 0;
+        auto take = [&](float x, int s) __attribute__((always_inline)) {
+            const float m = fabsf(x);
+            sgn ^= f2u(x);
+            if (m < min1) {
+                min2 = min1;
+                min1 = m;
+                idx = s;
+            } else if (m < min2) {
+                min2 = m;
             }
+        };
+        static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
+            constexpr int s = decltype(SS)::value;
+            if (s < R) {
+                v[s] = v[s] - ira_c2v(st, mt, s);
+                take(v[s], s);
+            }
+        });
+        const float vp0 = ap0 - ira_c2v(st, mt, kIPS);
+        const float vp1 = ap1 - ira_c2v(st, mt, kIPS + 1);
+        const bool has_prev = ra > 0 || p > 0;  // check 0 has no p_{-1}
+        take(vp0, kIPS);
+        if (has_prev) take(vp1, kIPS + 1);
+        const float mag1 = ms_mag(min1, alpha, beta, clamp);
+        const float mag2 = ms_mag(min2, alpha, beta, clamp);
+        uint32_t meta = (uint32_t)idx << 27;
+        static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
+            constexpr int s = decltype(SS)::value;
+            if (s < R) meta |= ((sgn ^ f2u(v[s])) >> 31) << s;
+        });
+        meta |= ((sgn ^ f2u(vp0)) >> 31) << kIPS;
+        if (has_prev) meta |= ((sgn ^ f2u(vp1)) >> 31) << (kIPS + 1);
+        if (pos < kIZ) {
+            S[si] = make_float2(mag1, mag2);
+            MT[si] = meta;
         }
     }
 }
@@ -460,21 +430,18 @@ size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {
     return 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8) + a256((size_t)bc * s->M * 4);
 }
 
-// positions per lane: IRA_PPL (compile-time; A/B on config [4], profiles/r05/ab/ab_c4_ira_ppl.txt: 1 fastest)
-#ifndef IRA_PPL
-#define IRA_PPL 1
-#endif
-static void ira_launch_vn(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* L, float* app,
-                          const float2* S, const uint32_t* MT, int b, int tpw) {
-    constexpr int NT = ira_threads<IRA_PPL>();
-    if (s->maxdv <= 8) k_ira_vn<8, IRA_PPL><<<g, NT, 0, st>>>(t, L, app, S, MT, b, tpw);
-    else k_ira_vn<16, IRA_PPL><<<g, NT, 0, st>>>(t, L, app, S, MT, b, tpw);
+// tasks side by side per workgroup (A/B knob LDPC_IRA_TPP: 1 or 2)
+template <int TPP>
+static void ira_vn_tpp(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* L, float* app,
+                       const float2* S, const uint32_t* MT, int b, int tpw) {
+    if (s->maxdv <= 8) k_ira_vn<8, TPP><<<g, kIraLanes * TPP, 0, st>>>(t, L, app, S, MT, b, tpw);
+    else k_ira_vn<16, TPP><<<g, kIraLanes * TPP, 0, st>>>(t, L, app, S, MT, b, tpw);
 }
-static void ira_launch_cn(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* app, float2* S,
-                          uint32_t* MT, int b, const ldpc_params& p, int tpw) {
-    constexpr int NT = ira_threads<IRA_PPL>();
-    if (s->maxr <= 8) k_ira_cn<8, IRA_PPL><<<g, NT, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
-    else k_ira_cn<kICS, IRA_PPL><<<g, NT, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
+template <int TPP>
+static void ira_cn_tpp(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* app, float2* S,
+                       uint32_t* MT, int b, const ldpc_params& p, int tpw) {
+    if (s->maxr <= 8) k_ira_cn<8, TPP><<<g, kIraLanes * TPP, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
+    else k_ira_cn<kICS, TPP><<<g, kIraLanes * TPP, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
 }
 
 int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params& p, uint8_t* bits, float* soft,
@@ -493,6 +460,8 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     // (config [4], 200 MB chunks), 16 tasks: 20.8k (too few workgroups)
     const char* tenv = getenv("LDPC_IRA_TPW");
     const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 4;
+    const char* penv = getenv("LDPC_IRA_TPP");
+    const int tpp = penv && atoi(penv) == 2 ? 2 : 1;
     for (int64_t o = 0; o < B; o += bc) {
         const int b = (int)(B - o < bc ? B - o : bc);
         const int64_t vo = o * s->n;
@@ -501,11 +470,14 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
         if (hipMemsetAsync(S, 0, (size_t)b * s->M * 8, st) != hipSuccess ||
             hipMemsetAsync(MT, 0, (size_t)b * s->M * 4, st) != hipSuccess)
             return set_error(LDPC_EHIP, "IRA state init failed");
-        const unsigned gvn = cw8 * (unsigned)((s->G + s->q + tpw - 1) / tpw), gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
+        const int per = tpw * tpp;
+        const unsigned gvn = cw8 * (unsigned)((s->G + s->q + per - 1) / per), gcn = cw8 * (unsigned)((s->q + per - 1) / per);
         for (int it = 0; it <= p.iters; ++it) {
-            ira_launch_vn(s, gvn, st, t, L, app, S, MT, b, tpw);
+            if (tpp == 2) ira_vn_tpp<2>(s, gvn, st, t, L, app, S, MT, b, tpw);
+            else ira_vn_tpp<1>(s, gvn, st, t, L, app, S, MT, b, tpw);
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
-            ira_launch_cn(s, gcn, st, t, app, S, MT, b, p, tpw);
+            if (tpp == 2) ira_cn_tpp<2>(s, gcn, st, t, app, S, MT, b, p, tpw);
+            else ira_cn_tpp<1>(s, gcn, st, t, app, S, MT, b, p, tpw);
         }
         k_ira_out<<<dim3(tiles, b), 256, 0, st>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
                                                   s->n, s->k, s->q);

@@ -84,19 +84,12 @@ __device__ __forceinline__ void rotate_left(float (&c)[D], int rho) {
     });
 }
 
-// Workgroup shape: TPP tasks side by side (kIraLanes threads each: 6 waves over the 360 positions, lanes past 360
-// repeat the last position and store nothing), each sub-group running `tpw` tasks one after the other.  Every load
-// of a task is issued before the first is used (a task waits on one memory round trip, not D).
+// Workgroup shape: one task at a time over kIraLanes threads (6 waves over the 360 positions; lanes past 360
+// repeat the last position and store nothing), `tpw` tasks one after the other.  Every load of a task is issued
+// before the first is used: a task waits on one memory round trip, not one per edge (A/B
+// profiles/r05/ab/ab_c4_ira_restructure.txt).  Two tasks side by side per workgroup measured no faster
+// (ab_c4_ira_tpp.txt), nor did several positions per lane (ab_c4_ira_ppl.txt).
 constexpr int kIraLanes = 384;
-
-template <int TPP>
-__device__ __forceinline__ int ira_pos() {
-    return TPP == 1 ? (int)threadIdx.x : (int)threadIdx.x % kIraLanes;
-}
-template <int TPP>
-__device__ __forceinline__ int ira_sub() {  // wave-uniform: kIraLanes is a multiple of 64
-    return TPP == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / kIraLanes);
-}
 
 // app of information variable (g, pos) of degree D: L + its c2v in ascending check order
 template <int D>
@@ -130,15 +123,15 @@ __device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int
 
 // One task = one variable group (information group g < G, or parity row a = g - G) of one codeword; lanes =
 // the 360 positions.  Writes app in the permuted layout (information: g*360 + m, parity: k + a*360 + b).
-template <int MAXDV, int TPP>
-__global__ __launch_bounds__(kIraLanes * TPP) void k_ira_vn(IRADev t, const float* __restrict__ L,
-                                                             float* __restrict__ app, const float2* __restrict__ S,
-                                                             const uint32_t* __restrict__ MT, int Bc, int tpw) {
-    const int T = t.G + t.q, per = tpw * TPP;
+template <int MAXDV>
+__global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __restrict__ L, float* __restrict__ app,
+                                                      const float2* __restrict__ S, const uint32_t* __restrict__ MT,
+                                                      int Bc, int tpw) {
+    const int T = t.G + t.q;
     int cw, tb;
-    if (!ira_task((T + per - 1) / per, Bc, cw, tb)) return;
-    const int pos = ira_pos<TPP>();
-    for (int gi = tb * per + ira_sub<TPP>(); gi < T && gi < (tb + 1) * per; gi += TPP) {
+    if (!ira_task((T + tpw - 1) / tpw, Bc, cw, tb)) return;
+    const int pos = threadIdx.x;
+    for (int gi = tb * tpw; gi < T && gi < (tb + 1) * tpw; ++gi) {
         const int64_t vo = (int64_t)cw * t.n + (int64_t)gi * kIZ;
         const int64_t so = (int64_t)cw * t.M;
         if (gi < t.G) {
@@ -171,16 +164,15 @@ __global__ __launch_bounds__(kIraLanes * TPP) void k_ira_vn(IRADev t, const floa
 
 // One task = one check row a of one codeword; lanes = positions b.  Reads the posteriors of the row's variables
 // and its own state, writes the new state (the oracle's k_cn_ms arithmetic on v2c = app - c2v).
-template <int MAXR, int TPP>
-__global__ __launch_bounds__(kIraLanes * TPP) void k_ira_cn(IRADev t, const float* __restrict__ app,
-                                                             float2* __restrict__ S, uint32_t* __restrict__ MT,
-                                                             int Bc, float clamp, float alpha, float beta, int tpw) {
-    const int per = tpw * TPP;
+template <int MAXR>
+__global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __restrict__ app, float2* __restrict__ S,
+                                                      uint32_t* __restrict__ MT, int Bc, float clamp, float alpha,
+                                                      float beta, int tpw) {
     int cw, tb;
-    if (!ira_task((t.q + per - 1) / per, Bc, cw, tb)) return;
-    const int pos = ira_pos<TPP>();
+    if (!ira_task((t.q + tpw - 1) / tpw, Bc, cw, tb)) return;
+    const int pos = threadIdx.x;
     const int p = min(pos, kIZ - 1);
-    for (int ra = tb * per + ira_sub<TPP>(); ra < t.q && ra < (tb + 1) * per; ra += TPP) {
+    for (int ra = tb * tpw; ra < t.q && ra < (tb + 1) * tpw; ++ra) {
         const int64_t ao = (int64_t)cw * t.n;
         const int64_t si = (int64_t)cw * t.M + (int64_t)ra * kIZ + p;
         const int R = t.cdeg[ra];
@@ -430,20 +422,6 @@ size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {
     return 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8) + a256((size_t)bc * s->M * 4);
 }
 
-// tasks side by side per workgroup (A/B knob LDPC_IRA_TPP: 1 or 2)
-template <int TPP>
-static void ira_vn_tpp(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* L, float* app,
-                       const float2* S, const uint32_t* MT, int b, int tpw) {
-    if (s->maxdv <= 8) k_ira_vn<8, TPP><<<g, kIraLanes * TPP, 0, st>>>(t, L, app, S, MT, b, tpw);
-    else k_ira_vn<16, TPP><<<g, kIraLanes * TPP, 0, st>>>(t, L, app, S, MT, b, tpw);
-}
-template <int TPP>
-static void ira_cn_tpp(const IRASpec* s, unsigned g, hipStream_t st, const IRADev& t, const float* app, float2* S,
-                       uint32_t* MT, int b, const ldpc_params& p, int tpw) {
-    if (s->maxr <= 8) k_ira_cn<8, TPP><<<g, kIraLanes * TPP, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
-    else k_ira_cn<kICS, TPP><<<g, kIraLanes * TPP, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
-}
-
 int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params& p, uint8_t* bits, float* soft,
                int32_t* iters_used, char* ws, hipStream_t st) {
     const int64_t bc = ira_chunk(s, B);
@@ -460,8 +438,6 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     // (config [4], 200 MB chunks), 16 tasks: 20.8k (too few workgroups)
     const char* tenv = getenv("LDPC_IRA_TPW");
     const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 4;
-    const char* penv = getenv("LDPC_IRA_TPP");
-    const int tpp = penv && atoi(penv) == 2 ? 2 : 1;
     for (int64_t o = 0; o < B; o += bc) {
         const int b = (int)(B - o < bc ? B - o : bc);
         const int64_t vo = o * s->n;
@@ -470,14 +446,13 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
         if (hipMemsetAsync(S, 0, (size_t)b * s->M * 8, st) != hipSuccess ||
             hipMemsetAsync(MT, 0, (size_t)b * s->M * 4, st) != hipSuccess)
             return set_error(LDPC_EHIP, "IRA state init failed");
-        const int per = tpw * tpp;
-        const unsigned gvn = cw8 * (unsigned)((s->G + s->q + per - 1) / per), gcn = cw8 * (unsigned)((s->q + per - 1) / per);
+        const unsigned gvn = cw8 * (unsigned)((s->G + s->q + tpw - 1) / tpw), gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
         for (int it = 0; it <= p.iters; ++it) {
-            if (tpp == 2) ira_vn_tpp<2>(s, gvn, st, t, L, app, S, MT, b, tpw);
-            else ira_vn_tpp<1>(s, gvn, st, t, L, app, S, MT, b, tpw);
+            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, kIraLanes, 0, st>>>(t, L, app, S, MT, b, tpw);
+            else k_ira_vn<16><<<gvn, kIraLanes, 0, st>>>(t, L, app, S, MT, b, tpw);
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
-            if (tpp == 2) ira_cn_tpp<2>(s, gcn, st, t, app, S, MT, b, p, tpw);
-            else ira_cn_tpp<1>(s, gcn, st, t, app, S, MT, b, p, tpw);
+            if (s->maxr <= 8) k_ira_cn<8><<<gcn, kIraLanes, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
+            else k_ira_cn<kICS><<<gcn, kIraLanes, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
         }
         k_ira_out<<<dim3(tiles, b), 256, 0, st>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
                                                   s->n, s->k, s->q);

@@ -113,7 +113,7 @@ def test_equals_generic_kernels_and_chunking(dvbs2, monkeypatch):
         monkeypatch.setenv("LDPC_IRA_TPW", tpw)
         bits, z, _ = _decode(dec, x, 12, clamp=20.0)
         assert np.array_equal(bits, gb) and _same(z, gz), tpw
-
+    monkeypatch.delenv("LDPC_IRA_TPW", raising=False)
 
 
 def test_shaped_code_and_host_pointers():

@@ -401,9 +401,9 @@ bool ira_supports(const IRASpec* s, const ldpc_params& p) {
 // codewords per chunk: each chunk's arrays (8n + 12M bytes per codeword) stay in the 256 MiB Infinity Cache for
 // all its iterations; LDPC_IRA_BUDGET_MB overrides (0 = the whole batch in one pass).  Config [4], B = 4,096
 // (profiles/r05/ab/ab_c4_ira_tpw.txt): 100 MB 28.2k cw/s, 200 MB 32.8k, 240 MB 33.6k, 256 MB 34.0k, 400 MB 25.2k.
-static int64_t ira_chunk(const IRASpec* s, int64_t B) {
+static int64_t ira_chunk(const IRASpec* s, int64_t B, int ns = 1) {
     const char* env = getenv("LDPC_IRA_BUDGET_MB");
-    const int64_t budget = (env ? (int64_t)atol(env) : 256) << 20;
+    const int64_t budget = ((env ? (int64_t)atol(env) : 256) << 20) / ns;
     if (budget <= 0) return B;
     const int64_t per = 8 * (int64_t)s->n + 12 * (int64_t)s->M;
     int64_t bc = budget / per / 8 * 8;
@@ -416,20 +416,28 @@ static int64_t ira_chunk(const IRASpec* s, int64_t B) {
     return eq < bc ? eq : bc;
 }
 
-size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {
-    const int64_t bc = ira_chunk(s, B);
+// chunks decoded side by side on two streams (the caller's and a forked one), each half the budget: LDPC_IRA_STREAMS
+static int ira_streams() {
+    const char* e = getenv("LDPC_IRA_STREAMS");
+    return (e && atoi(e) == 2) ? 2 : 1;
+}
+
+static size_t ira_set_bytes(const IRASpec* s, int64_t bc) {  // L, app, S, MT of bc codewords
     auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     return 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8) + a256((size_t)bc * s->M * 4);
 }
 
+size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {
+    const int ns = ira_streams();
+    return (size_t)ns * ira_set_bytes(s, ira_chunk(s, B, ns));
+}
+
 int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params& p, uint8_t* bits, float* soft,
                int32_t* iters_used, char* ws, hipStream_t st) {
-    const int64_t bc = ira_chunk(s, B);
+    const int ns = ira_streams();
+    const int64_t bc = ira_chunk(s, B, ns);
+    const size_t set = ira_set_bytes(s, bc);
     auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    float* L = (float*)ws;
-    float* app = (float*)(ws + a256((size_t)bc * s->n * 4));
-    float2* S = (float2*)(ws + 2 * a256((size_t)bc * s->n * 4));
-    uint32_t* MT = (uint32_t*)(ws + 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8));
     const IRADev t{s->vn, s->vdeg, s->cn, s->cdeg, s->q, s->G, s->k, s->n, s->M};
     const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
     const unsigned tiles = (unsigned)((s->k + 1023) / 1024 + ((kIZ + 63) / 64) * ((s->q + 63) / 64));
@@ -438,25 +446,38 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     // (config [4], 200 MB chunks), 16 tasks: 20.8k (too few workgroups)
     const char* tenv = getenv("LDPC_IRA_TPW");
     const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 4;
-    for (int64_t o = 0; o < B; o += bc) {
+    hipStream_t str[2] = {st, st};
+    if (ns == 2 && B > bc)
+        if (const int rc = aux_fork(st, &str[1])) return rc;
+    int i = 0;
+    for (int64_t o = 0; o < B; o += bc, ++i) {
+        const int k = ns == 2 ? (i & 1) : 0;
+        hipStream_t q = str[k];
+        char* w = ws + (size_t)k * set;
+        float* L = (float*)w;
+        float* app = (float*)(w + a256((size_t)bc * s->n * 4));
+        float2* S = (float2*)(w + 2 * a256((size_t)bc * s->n * 4));
+        uint32_t* MT = (uint32_t*)(w + 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8));
         const int b = (int)(B - o < bc ? B - o : bc);
         const int64_t vo = o * s->n;
         const unsigned cw8 = (unsigned)((b + 7) / 8) * 8;
-        k_ira_load<<<dim3(tiles, b), 256, 0, st>>>(llr + vo, L, s->n, s->k, s->q);
-        if (hipMemsetAsync(S, 0, (size_t)b * s->M * 8, st) != hipSuccess ||
-            hipMemsetAsync(MT, 0, (size_t)b * s->M * 4, st) != hipSuccess)
+        k_ira_load<<<dim3(tiles, b), 256, 0, q>>>(llr + vo, L, s->n, s->k, s->q);
+        if (hipMemsetAsync(S, 0, (size_t)b * s->M * 8, q) != hipSuccess ||
+            hipMemsetAsync(MT, 0, (size_t)b * s->M * 4, q) != hipSuccess)
             return set_error(LDPC_EHIP, "IRA state init failed");
         const unsigned gvn = cw8 * (unsigned)((s->G + s->q + tpw - 1) / tpw), gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
         for (int it = 0; it <= p.iters; ++it) {
-            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, kIraLanes, 0, st>>>(t, L, app, S, MT, b, tpw);
-            else k_ira_vn<16><<<gvn, kIraLanes, 0, st>>>(t, L, app, S, MT, b, tpw);
+            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, MT, b, tpw);
+            else k_ira_vn<16><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, MT, b, tpw);
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
-            if (s->maxr <= 8) k_ira_cn<8><<<gcn, kIraLanes, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
-            else k_ira_cn<kICS><<<gcn, kIraLanes, 0, st>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
+            if (s->maxr <= 8) k_ira_cn<8><<<gcn, kIraLanes, 0, q>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
+            else k_ira_cn<kICS><<<gcn, kIraLanes, 0, q>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
         }
-        k_ira_out<<<dim3(tiles, b), 256, 0, st>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
-                                                  s->n, s->k, s->q);
+        k_ira_out<<<dim3(tiles, b), 256, 0, q>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
+                                                 s->n, s->k, s->q);
     }
+    if (ns == 2 && B > bc)
+        if (const int rc = aux_join(st)) return rc;
     if (iters_used) fill_i32(iters_used, B, p.iters, st);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "IRA kernel launch: %s", hipGetErrorString(e));

@@ -1687,15 +1687,15 @@ __global__ __launch_bounds__(256) void k_sp_zero_scan(const float* __restrict__ 
 }
 
 namespace {
-struct SpAux {  // per host thread and device: the second stream and the fork / join events
+struct Aux {  // per host thread and device: the second stream and the fork / join events
     hipStream_t s2 = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
 };
-SpAux* sp_aux() {
-    static thread_local SpAux aux[64];
+Aux* aux_get() {
+    static thread_local Aux aux[64];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    SpAux& a = aux[dev];
+    Aux& a = aux[dev];
     if (!a.join) {
         if (!a.s2 && hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking) != hipSuccess) {
             a.s2 = nullptr;
@@ -1714,25 +1714,32 @@ SpAux* sp_aux() {
 }
 }  // namespace
 
-int qc_sp_fork(const float* llr, int64_t B, int n, int cpu, hipStream_t st, hipStream_t* s2) {
-    uint32_t* zl = qc_sp_zlist();
-    SpAux* a = sp_aux();
-    if (!zl || !a) return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: no workspace or auxiliary stream");
-    if (hipMemsetAsync(zl, 0, 4, st) != hipSuccess) return set_error(LDPC_EHIP, "zero-LLR list reset failed");
-    const int64_t units = (B + cpu - 1) / cpu;
-    k_sp_zero_scan<<<(unsigned)((units + 3) / 4), 256, 0, st>>>(llr, B, n, cpu, units, zl);
+int aux_fork(hipStream_t st, hipStream_t* s2) {
+    Aux* a = aux_get();
+    if (!a) return set_error(LDPC_EHIP, "auxiliary stream unavailable");
     if (hipEventRecord(a->fork, st) != hipSuccess || hipStreamWaitEvent(a->s2, a->fork, 0) != hipSuccess)
-        return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: stream fork failed");
+        return set_error(LDPC_EHIP, "auxiliary stream: fork failed");
     *s2 = a->s2;
     return LDPC_OK;
 }
 
-int qc_sp_join(hipStream_t st) {
-    SpAux* a = sp_aux();
+int aux_join(hipStream_t st) {
+    Aux* a = aux_get();
     if (!a || hipEventRecord(a->join, a->s2) != hipSuccess || hipStreamWaitEvent(st, a->join, 0) != hipSuccess)
-        return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: stream join failed");
+        return set_error(LDPC_EHIP, "auxiliary stream: join failed");
     return LDPC_OK;
 }
+
+int qc_sp_fork(const float* llr, int64_t B, int n, int cpu, hipStream_t st, hipStream_t* s2) {
+    uint32_t* zl = qc_sp_zlist();
+    if (!zl) return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: no workspace");
+    if (hipMemsetAsync(zl, 0, 4, st) != hipSuccess) return set_error(LDPC_EHIP, "zero-LLR list reset failed");
+    const int64_t units = (B + cpu - 1) / cpu;
+    k_sp_zero_scan<<<(unsigned)((units + 3) / 4), 256, 0, st>>>(llr, B, n, cpu, units, zl);
+    return aux_fork(st, s2);
+}
+
+int qc_sp_join(hipStream_t st) { return aux_join(st); }
 
 int qc_decode(const QCSpec* s, const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft,
               int32_t* used, char* ws, hipStream_t st) {

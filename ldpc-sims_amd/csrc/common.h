@@ -494,10 +494,10 @@ __host__ __device__ inline uint8_t* qc_sp_zflag(uint32_t* zlist, int64_t B) {
 }
 int qc_sp_fork(const float* llr, int64_t B, int n, int cpu, hipStream_t st, hipStream_t* s2);
 int qc_sp_join(hipStream_t st);
-// a second stream per host thread and device, forked from / joined back into the caller's stream by events
+// up to 3 extra streams per host thread and device, forked from / joined back into the caller's stream by events
 // (graph-capturable); one fork / join pair at a time per thread (qc.hip)
-int aux_fork(hipStream_t st, hipStream_t* s2);
-int aux_join(hipStream_t st);
+int aux_fork(hipStream_t st, hipStream_t* s2, int n = 1);
+int aux_join(hipStream_t st, int n = 1);
 constexpr unsigned kSpPass2Blocks = 1280;  // second-pass grid cap: 5 units per CU
 inline unsigned qc_sp_pass2_grid(unsigned blocks) { return blocks < kSpPass2Blocks ? blocks : kSpPass2Blocks; }
 

@@ -416,10 +416,12 @@ static int64_t ira_chunk(const IRASpec* s, int64_t B, int ns = 1) {
     return eq < bc ? eq : bc;
 }
 
-// chunks decoded side by side on two streams (the caller's and a forked one), each half the budget: LDPC_IRA_STREAMS
+// chunks decoded side by side on NS streams (the caller's and NS - 1 forked ones), each 1/NS of the budget
+// (LDPC_IRA_STREAMS, 1..4)
 static int ira_streams() {
     const char* e = getenv("LDPC_IRA_STREAMS");
-    return (e && atoi(e) == 2) ? 2 : 1;
+    const int v = e ? atoi(e) : 1;
+    return v < 1 ? 1 : (v > 4 ? 4 : v);
 }
 
 static size_t ira_set_bytes(const IRASpec* s, int64_t bc) {  // L, app, S, MT of bc codewords
@@ -446,12 +448,14 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     // (config [4], 200 MB chunks), 16 tasks: 20.8k (too few workgroups)
     const char* tenv = getenv("LDPC_IRA_TPW");
     const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 4;
-    hipStream_t str[2] = {st, st};
-    if (ns == 2 && B > bc)
-        if (const int rc = aux_fork(st, &str[1])) return rc;
+    hipStream_t str[4] = {st, st, st, st};
+    const int nch = (int)((B + bc - 1) / bc);
+    const int nf = (ns < nch ? ns : nch) - 1;  // forked streams in use
+    if (nf > 0)
+        if (const int rc = aux_fork(st, &str[1], nf)) return rc;
     int i = 0;
     for (int64_t o = 0; o < B; o += bc, ++i) {
-        const int k = ns == 2 ? (i & 1) : 0;
+        const int k = i % (nf + 1);
         hipStream_t q = str[k];
         char* w = ws + (size_t)k * set;
         float* L = (float*)w;
@@ -476,8 +480,8 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
         k_ira_out<<<dim3(tiles, b), 256, 0, q>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
                                                  s->n, s->k, s->q);
     }
-    if (ns == 2 && B > bc)
-        if (const int rc = aux_join(st)) return rc;
+    if (nf > 0)
+        if (const int rc = aux_join(st, nf)) return rc;
     if (iters_used) fill_i32(iters_used, B, p.iters, st);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "IRA kernel launch: %s", hipGetErrorString(e));

@@ -1687,46 +1687,56 @@ __global__ __launch_bounds__(256) void k_sp_zero_scan(const float* __restrict__ 
 }
 
 namespace {
-struct Aux {  // per host thread and device: the second stream and the fork / join events
-    hipStream_t s2 = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+constexpr int kAux = 3;
+struct Aux {  // per host thread and device: kAux extra streams and their fork / join events
+    hipStream_t s[kAux] = {};
+    hipEvent_t fork = nullptr, join[kAux] = {};
+    bool ready = false;
 };
 Aux* aux_get() {
     static thread_local Aux aux[64];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
     Aux& a = aux[dev];
-    if (!a.join) {
-        if (!a.s2 && hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking) != hipSuccess) {
-            a.s2 = nullptr;
-            return nullptr;
-        }
+    if (!a.ready) {
         if (!a.fork && hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) != hipSuccess) {
             a.fork = nullptr;
             return nullptr;
         }
-        if (hipEventCreateWithFlags(&a.join, hipEventDisableTiming) != hipSuccess) {
-            a.join = nullptr;
-            return nullptr;
+        for (int i = 0; i < kAux; ++i) {
+            if (!a.s[i] && hipStreamCreateWithFlags(&a.s[i], hipStreamNonBlocking) != hipSuccess) {
+                a.s[i] = nullptr;
+                return nullptr;
+            }
+            if (!a.join[i] && hipEventCreateWithFlags(&a.join[i], hipEventDisableTiming) != hipSuccess) {
+                a.join[i] = nullptr;
+                return nullptr;
+            }
         }
+        a.ready = true;
     }
     return &a;
 }
 }  // namespace
 
-int aux_fork(hipStream_t st, hipStream_t* s2) {
+int aux_fork(hipStream_t st, hipStream_t* s2, int n) {
     Aux* a = aux_get();
-    if (!a) return set_error(LDPC_EHIP, "auxiliary stream unavailable");
-    if (hipEventRecord(a->fork, st) != hipSuccess || hipStreamWaitEvent(a->s2, a->fork, 0) != hipSuccess)
-        return set_error(LDPC_EHIP, "auxiliary stream: fork failed");
-    *s2 = a->s2;
+    if (!a || n < 1 || n > kAux) return set_error(LDPC_EHIP, "auxiliary streams unavailable");
+    if (hipEventRecord(a->fork, st) != hipSuccess) return set_error(LDPC_EHIP, "auxiliary stream: fork failed");
+    for (int i = 0; i < n; ++i) {
+        if (hipStreamWaitEvent(a->s[i], a->fork, 0) != hipSuccess)
+            return set_error(LDPC_EHIP, "auxiliary stream: fork failed");
+        s2[i] = a->s[i];
+    }
     return LDPC_OK;
 }
 
-int aux_join(hipStream_t st) {
+int aux_join(hipStream_t st, int n) {
     Aux* a = aux_get();
-    if (!a || hipEventRecord(a->join, a->s2) != hipSuccess || hipStreamWaitEvent(st, a->join, 0) != hipSuccess)
-        return set_error(LDPC_EHIP, "auxiliary stream: join failed");
+    if (!a || n < 1 || n > kAux) return set_error(LDPC_EHIP, "auxiliary streams unavailable");
+    for (int i = 0; i < n; ++i)
+        if (hipEventRecord(a->join[i], a->s[i]) != hipSuccess || hipStreamWaitEvent(st, a->join[i], 0) != hipSuccess)
+            return set_error(LDPC_EHIP, "auxiliary stream: join failed");
     return LDPC_OK;
 }
 

@@ -114,14 +114,15 @@ def test_equals_generic_kernels_and_chunking(dvbs2, monkeypatch):
         bits, z, _ = _decode(dec, x, 12, clamp=20.0)
         assert np.array_equal(bits, gb) and _same(z, gz), tpw
     monkeypatch.delenv("LDPC_IRA_TPW", raising=False)
-    monkeypatch.setenv("LDPC_IRA_STREAMS", "2")  # chunks alternating over two streams
-    for budget in ("1", "5", None):
-        if budget is None:
-            monkeypatch.delenv("LDPC_IRA_BUDGET_MB", raising=False)
-        else:
-            monkeypatch.setenv("LDPC_IRA_BUDGET_MB", budget)
-        bits, z, _ = _decode(dec, x, 12, clamp=20.0)
-        assert np.array_equal(bits, gb) and _same(z, gz), ("streams", budget)
+    for ns in ("1", "2", "3", "4"):  # chunks round-robin over ns streams
+        monkeypatch.setenv("LDPC_IRA_STREAMS", ns)
+        for budget in ("1", "5", None):
+            if budget is None:
+                monkeypatch.delenv("LDPC_IRA_BUDGET_MB", raising=False)
+            else:
+                monkeypatch.setenv("LDPC_IRA_BUDGET_MB", budget)
+            bits, z, _ = _decode(dec, x, 12, clamp=20.0)
+            assert np.array_equal(bits, gb) and _same(z, gz), (ns, budget)
     monkeypatch.delenv("LDPC_IRA_STREAMS", raising=False)
     monkeypatch.delenv("LDPC_IRA_BUDGET_MB", raising=False)
 

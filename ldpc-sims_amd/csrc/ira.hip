@@ -398,12 +398,13 @@ bool ira_supports(const IRASpec* s, const ldpc_params& p) {
     return s->maxdv <= 16 && s->maxr <= kICS;
 }
 
-// codewords per chunk: each chunk's arrays (8n + 12M bytes per codeword) stay in the 256 MiB Infinity Cache for
-// all its iterations; LDPC_IRA_BUDGET_MB overrides (0 = the whole batch in one pass).  Config [4], B = 4,096
-// (profiles/r05/ab/ab_c4_ira_tpw.txt): 100 MB 28.2k cw/s, 200 MB 32.8k, 240 MB 33.6k, 256 MB 34.0k, 400 MB 25.2k.
+// codewords per chunk: the arrays of the chunks in flight (8n + 12M bytes per codeword) stay in the 256 MiB
+// Infinity Cache for all their iterations; LDPC_IRA_BUDGET_MB overrides (0 = the whole batch in one pass).  Config
+// [4], B = 4,096, one stream (profiles/r05/ab/ab_c4_ira_tpw.txt): 100 MB 28.2k cw/s, 200 MB 32.8k, 240 MB 33.6k,
+// 256 MB 34.0k, 400 MB 25.2k; two streams: 200 MB 41.55k, 256 MB 41.3k, 320 MB 35.5k (ab_c4_ira_streams.txt).
 static int64_t ira_chunk(const IRASpec* s, int64_t B, int ns = 1) {
     const char* env = getenv("LDPC_IRA_BUDGET_MB");
-    const int64_t budget = ((env ? (int64_t)atol(env) : 256) << 20) / ns;
+    const int64_t budget = ((env ? (int64_t)atol(env) : 200) << 20) / ns;
     if (budget <= 0) return B;
     const int64_t per = 8 * (int64_t)s->n + 12 * (int64_t)s->M;
     int64_t bc = budget / per / 8 * 8;
@@ -417,10 +418,12 @@ static int64_t ira_chunk(const IRASpec* s, int64_t B, int ns = 1) {
 }
 
 // chunks decoded side by side on NS streams (the caller's and NS - 1 forked ones), each 1/NS of the budget
-// (LDPC_IRA_STREAMS, 1..4)
+// (LDPC_IRA_STREAMS, 1..4).  Two kernels of different chunks fill each other's ramp, drain and latency gaps:
+// config [4] 38.3 -> 41.3-41.6k cw/s with 2 streams, 41.6-41.8k with 3, 41.2k with 4
+// (profiles/r05/ab/ab_c4_ira_streams.txt); 2 shipped.
 static int ira_streams() {
     const char* e = getenv("LDPC_IRA_STREAMS");
-    const int v = e ? atoi(e) : 1;
+    const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : (v > 4 ? 4 : v);
 }
 

@@ -58,8 +58,10 @@ def per_kernel(path):
 def trace_durations(path):
     """{kernel name: [(dispatch id, duration ms)]} from the kernel-trace pass."""
     out = {}
-    for f in glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True):
-        for t in csv.DictReader(open(f)):
+    files = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
+    files += glob.glob(os.path.join(path, "**", "*kernel_trace.csv.gz"), recursive=True)  # committed copies
+    for f in files:
+        for t in csv.DictReader(gzip.open(f, "rt") if f.endswith(".gz") else open(f)):
             out.setdefault(t["Kernel_Name"], []).append(
                 (int(t["Dispatch_Id"]), (int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) / 1e6))
     return {k: sorted(v) for k, v in out.items()}
@@ -77,7 +79,10 @@ def summarise(vals, durs, kernel=None, decode_kernels=None, last=0, chunks=1):
         names = {k for (k, _) in vals if kernel in k}
         if not names:
             raise SystemExit(f"no kernel matching {kernel}")
-        kname = max(names, key=lambda k: sum(map(len, vals.get((k, "SQ_INSTS_VALU"), vals.get((k, "FETCH_SIZE"), [])))))
+        # the kernel doing the work: most VALU instructions (FETCH_SIZE if no pass counted VALU), not most
+        # dispatches — a two-pass decode (the tanh-SP zero pass) dispatches both kernels equally often
+        kname = max(sorted(names), key=lambda k: sum(v for pas in vals.get((k, "SQ_INSTS_VALU"), vals.get((k, "FETCH_SIZE"), []))
+                                                     for _, v in pas))
         c = {cn: statistics.fmean(statistics.fmean(_tail(rows, last)) for rows in passes)
              for (k, cn), passes in vals.items() if k == kname}
         d = _tail(durs.get(kname, []), last)
@@ -164,9 +169,15 @@ def main():
             d["awgn_fetch_kb_x2"] = 2 * statistics.fmean(_tail(vals[(aw[0], "FETCH_SIZE")][0], 0))
             d["awgn_write_kb"] = statistics.fmean(_tail(vals[(aw[0], "WRITE_SIZE")][0], 0))
     rec["derived"] = d
-    # a multi-launch decode (~500 dispatches) adds each dispatch's few us of front-end time to the counter's
-    # window but not to the kernels' traced durations: 3 % there
-    tol = CLOCK_TOL if a.kernel else 1.03
+    # a multi-launch decode adds each dispatch's few us of front-end time to the counter's window but not to the
+    # kernels' traced durations: 3 % at ~500 dispatches (the generic kernels), more for the IRA decode's ~1,900;
+    # allowed: 8 us per dispatch on top of 3 % (counting the wrong launches would still be 2x off)
+    if a.kernel:
+        tol = CLOCK_TOL
+    else:
+        per_dec = sum(v["calls"] for v in ks["per_kernel"].values()) / max(1, ks["calls"])
+        tol = 1.03 + (per_dec * 8e-3 / ks["mean_ms"] if ks.get("mean_ms") else 0.0)
+        d["dispatches_per_decode"] = per_dec
     if d.get("clock_ghz", 0.0) > a.max_clock_ghz * tol:
         raise SystemExit(f"REJECTED {a.name}: implied clock {d['clock_ghz']:.3f} GHz > {a.max_clock_ghz} GHz — the "
                          f"counted launches are not the timed ones")

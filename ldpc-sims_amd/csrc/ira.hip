@@ -51,9 +51,18 @@ struct IRADev {
 };
 
 // c2v of slot `slot` from a check state: the argmin slot gets mag2, every other mag1; sign bit from meta
-__device__ __forceinline__ float ira_c2v(float2 st, uint32_t mt, int slot) {
-    const float mag = ((mt >> 27) == (uint32_t)slot) ? st.y : st.x;
-    return u2f(f2u(mag) | ((mt << (31 - slot)) & 0x80000000u));
+// One check's state, 12 bytes read and written as one dwordx3: the two output magnitudes and the meta word
+struct IraState {
+    float m1, m2;
+    uint32_t meta;
+};
+static_assert(sizeof(IraState) == 12, "one dwordx3 per check state");
+
+__device__ __forceinline__ IraState ira_ld(const IraState* __restrict__ p) { return *p; }
+
+__device__ __forceinline__ float ira_c2v(const IraState& st, int slot) {
+    const float mag = ((st.meta >> 27) == (uint32_t)slot) ? st.m2 : st.m1;
+    return u2f(f2u(mag) | ((st.meta << (31 - slot)) & 0x80000000u));
 }
 
 // Workgroup b -> (codeword, task): blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch),
@@ -94,8 +103,8 @@ constexpr int kIraLanes = 384;
 // app of information variable (g, pos) of degree D: L + its c2v in ascending check order
 template <int D>
 __device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int64_t vo, int64_t so, int pos,
-                                            const float* __restrict__ L, const float2* __restrict__ S,
-                                            const uint32_t* __restrict__ MT, float* __restrict__ app) {
+                                            const float* __restrict__ L, const IraState* __restrict__ S,
+                                            float* __restrict__ app) {
     const int p = min(pos, kIZ - 1);
     const float a = L[vo + p];
     float c[D];
@@ -109,7 +118,7 @@ __device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int
         b -= w ? kIZ : 0;
         wrapped += w;
         const int64_t i = so + (int64_t)ra * kIZ + b;
-        c[t] = ira_c2v(S[i], MT[i], slot);
+        c[t] = ira_c2v(ira_ld(S + i), slot);
     });
     // entries are sorted by x = a + q s, i.e. by s: the wrapped ones are the last `wrapped` entries and their
     // checks come first in ascending order
@@ -125,7 +134,7 @@ __device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int
 // the 360 positions.  Writes app in the permuted layout (information: g*360 + m, parity: k + a*360 + b).
 template <int MAXDV>
 __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __restrict__ L, float* __restrict__ app,
-                                                      const float2* __restrict__ S, const uint32_t* __restrict__ MT,
+                                                      const IraState* __restrict__ S,
                                                       int Bc, int tpw) {
     const int T = t.G + t.q;
     int cw, tb;
@@ -139,7 +148,7 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
             const int32_t* row = t.vn + gi * kIVS;
             static_for<1, MAXDV + 1>([&](auto DD) __attribute__((always_inline)) {
                 constexpr int D = decltype(DD)::value;
-                if (d == D) ira_vn_info<D>(row, vo, so, pos, L, S, MT, app);
+                if (d == D) ira_vn_info<D>(row, vo, so, pos, L, S, app);
             });
         } else {
             // parity p_j, j = r + q pos: checks j (its own (r, pos), slot kIPS) and j + 1 (slot kIPS + 1 there)
@@ -154,8 +163,8 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
             }
             const bool has1 = p1 < kIZ;  // j + 1 < M
             const int64_t i1 = so + (int64_t)r1 * kIZ + (has1 ? p1 : 0);
-            const float c0 = ira_c2v(S[i0], MT[i0], kIPS);
-            const float x1 = ira_c2v(S[i1], MT[i1], kIPS + 1);
+            const float c0 = ira_c2v(ira_ld(S + i0), kIPS);
+            const float x1 = ira_c2v(ira_ld(S + i1), kIPS + 1);
             const float c1 = has1 ? x1 : -0.0f;  // x + (-0) == x bit for bit: the last parity has one check
             if (pos < kIZ) app[vo + pos] = (a + c0) + c1;
         }
@@ -165,8 +174,8 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
 // One task = one check row a of one codeword; lanes = positions b.  Reads the posteriors of the row's variables
 // and its own state, writes the new state (the oracle's k_cn_ms arithmetic on v2c = app - c2v).
 template <int MAXR>
-__global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __restrict__ app, float2* __restrict__ S,
-                                                      uint32_t* __restrict__ MT, int Bc, float clamp, float alpha,
+__global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __restrict__ app,
+                                                      IraState* __restrict__ S, int Bc, float clamp, float alpha,
                                                       float beta, int tpw) {
     int cw, tb;
     if (!ira_task((t.q + tpw - 1) / tpw, Bc, cw, tb)) return;
@@ -177,8 +186,7 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
         const int64_t si = (int64_t)cw * t.M + (int64_t)ra * kIZ + p;
         const int R = t.cdeg[ra];
         const int32_t* row = t.cn + ra * kICS;
-        const float2 st = S[si];
-        const uint32_t mt = MT[si];
+        const IraState st = ira_ld(S + si);
         const float ap0 = app[ao + t.k + (int64_t)ra * kIZ + p];
         const int64_t pi = ra > 0 ? ao + t.k + (int64_t)(ra - 1) * kIZ + p
                                   : ao + t.k + (int64_t)(t.q - 1) * kIZ + (p > 0 ? p - 1 : 0);
@@ -211,12 +219,12 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
         static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
             constexpr int s = decltype(SS)::value;
             if (s < R) {
-                v[s] = v[s] - ira_c2v(st, mt, s);
+                v[s] = v[s] - ira_c2v(st, s);
                 take(v[s], s);
             }
         });
-        const float vp0 = ap0 - ira_c2v(st, mt, kIPS);
-        const float vp1 = ap1 - ira_c2v(st, mt, kIPS + 1);
+        const float vp0 = ap0 - ira_c2v(st, kIPS);
+        const float vp1 = ap1 - ira_c2v(st, kIPS + 1);
         const bool has_prev = ra > 0 || p > 0;  // check 0 has no p_{-1}
         take(vp0, kIPS);
         if (has_prev) take(vp1, kIPS + 1);
@@ -230,8 +238,7 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
         meta |= ((sgn ^ f2u(vp0)) >> 31) << kIPS;
         if (has_prev) meta |= ((sgn ^ f2u(vp1)) >> 31) << (kIPS + 1);
         if (pos < kIZ) {
-            S[si] = make_float2(mag1, mag2);
-            MT[si] = meta;
+            S[si] = IraState{mag1, mag2, meta};
         }
     }
 }
@@ -427,9 +434,9 @@ static int ira_streams() {
     return v < 1 ? 1 : (v > 4 ? 4 : v);
 }
 
-static size_t ira_set_bytes(const IRASpec* s, int64_t bc) {  // L, app, S, MT of bc codewords
+static size_t ira_set_bytes(const IRASpec* s, int64_t bc) {  // L, app, check states of bc codewords
     auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    return 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8) + a256((size_t)bc * s->M * 4);
+    return 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * sizeof(IraState));
 }
 
 size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {
@@ -463,22 +470,20 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
         char* w = ws + (size_t)k * set;
         float* L = (float*)w;
         float* app = (float*)(w + a256((size_t)bc * s->n * 4));
-        float2* S = (float2*)(w + 2 * a256((size_t)bc * s->n * 4));
-        uint32_t* MT = (uint32_t*)(w + 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * 8));
+        IraState* S = (IraState*)(w + 2 * a256((size_t)bc * s->n * 4));
         const int b = (int)(B - o < bc ? B - o : bc);
         const int64_t vo = o * s->n;
         const unsigned cw8 = (unsigned)((b + 7) / 8) * 8;
         k_ira_load<<<dim3(tiles, b), 256, 0, q>>>(llr + vo, L, s->n, s->k, s->q);
-        if (hipMemsetAsync(S, 0, (size_t)b * s->M * 8, q) != hipSuccess ||
-            hipMemsetAsync(MT, 0, (size_t)b * s->M * 4, q) != hipSuccess)
+        if (hipMemsetAsync(S, 0, (size_t)b * s->M * sizeof(IraState), q) != hipSuccess)
             return set_error(LDPC_EHIP, "IRA state init failed");
         const unsigned gvn = cw8 * (unsigned)((s->G + s->q + tpw - 1) / tpw), gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
         for (int it = 0; it <= p.iters; ++it) {
-            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, MT, b, tpw);
-            else k_ira_vn<16><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, MT, b, tpw);
+            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, b, tpw);
+            else k_ira_vn<16><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, b, tpw);
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
-            if (s->maxr <= 8) k_ira_cn<8><<<gcn, kIraLanes, 0, q>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
-            else k_ira_cn<kICS><<<gcn, kIraLanes, 0, q>>>(t, app, S, MT, b, p.clamp, p.alpha, p.beta, tpw);
+            if (s->maxr <= 8) k_ira_cn<8><<<gcn, kIraLanes, 0, q>>>(t, app, S, b, p.clamp, p.alpha, p.beta, tpw);
+            else k_ira_cn<kICS><<<gcn, kIraLanes, 0, q>>>(t, app, S, b, p.clamp, p.alpha, p.beta, tpw);
         }
         k_ira_out<<<dim3(tiles, b), 256, 0, q>>>(app, bits ? bits + vo : nullptr, soft ? soft + vo : nullptr, soft_z,
                                                  s->n, s->k, s->q);

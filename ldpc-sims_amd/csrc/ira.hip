@@ -453,11 +453,18 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     const IRADev t{s->vn, s->vdeg, s->cn, s->cdeg, s->q, s->G, s->k, s->n, s->M};
     const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
     const unsigned tiles = (unsigned)((s->k + 1023) / 1024 + ((kIZ + 63) / 64) * ((s->q + 63) / 64));
-    // tasks per workgroup: one task is a short wave (a few loads, one store), and at one task per workgroup the
-    // launch is bound by the workgroup dispatch rate (5 resident waves per CU, of 32); 4 tasks: 28.8k -> 33.0k cw/s
-    // (config [4], 200 MB chunks), 16 tasks: 20.8k (too few workgroups)
-    const char* tenv = getenv("LDPC_IRA_TPW");
-    const int tpw = tenv && atoi(tenv) > 0 ? atoi(tenv) : 4;
+    // tasks per workgroup: one task is a short wave (a few loads, one store); at one task per workgroup a launch is
+    // ~40 k short workgroups: 4 tasks took config [4] 28.8k -> 33.0k cw/s (200 MB chunks), 16 tasks 20.8k (too few
+    // workgroups) — profiles/r05/ab/ab_c4_ira_tpw.txt
+    // per kernel: VN 4, CN 6 (a divisor of q = 90 for DVB-S2 1/2; A/B profiles/r05/ab/ab_c4_ira_tpw_split.txt);
+    // LDPC_IRA_TPW sets both, LDPC_IRA_TPW_VN / _CN one
+    auto env_int = [](const char* name, int dflt) {
+        const char* e = getenv(name);
+        return e && atoi(e) > 0 ? atoi(e) : dflt;
+    };
+    const int tp_all = env_int("LDPC_IRA_TPW", 0);
+    const int tpv = env_int("LDPC_IRA_TPW_VN", tp_all ? tp_all : 4);
+    const int tpw = env_int("LDPC_IRA_TPW_CN", tp_all ? tp_all : 6);
     hipStream_t str[4] = {st, st, st, st};
     const int nch = (int)((B + bc - 1) / bc);
     const int nf = (ns < nch ? ns : nch) - 1;  // forked streams in use
@@ -477,10 +484,10 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
         k_ira_load<<<dim3(tiles, b), 256, 0, q>>>(llr + vo, L, s->n, s->k, s->q);
         if (hipMemsetAsync(S, 0, (size_t)b * s->M * sizeof(IraState), q) != hipSuccess)
             return set_error(LDPC_EHIP, "IRA state init failed");
-        const unsigned gvn = cw8 * (unsigned)((s->G + s->q + tpw - 1) / tpw), gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
+        const unsigned gvn = cw8 * (unsigned)((s->G + s->q + tpv - 1) / tpv), gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
         for (int it = 0; it <= p.iters; ++it) {
-            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, b, tpw);
-            else k_ira_vn<16><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, b, tpw);
+            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, b, tpv);
+            else k_ira_vn<16><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, b, tpv);
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
             if (s->maxr <= 8) k_ira_cn<8><<<gcn, kIraLanes, 0, q>>>(t, app, S, b, p.clamp, p.alpha, p.beta, tpw);
             else k_ira_cn<kICS><<<gcn, kIraLanes, 0, q>>>(t, app, S, b, p.clamp, p.alpha, p.beta, tpw);

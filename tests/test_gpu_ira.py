@@ -140,6 +140,20 @@ def test_shaped_code_and_host_pointers():
     assert _same(r["soft"], g["soft"])
 
 
+def test_host_pointers_with_forked_chunks(dvbs2, monkeypatch):
+    """Host pointers (staged through the library's workspace; Decoder.decode and ldpc_amd.decode) with several
+    Infinity-Cache chunks on two streams: the forked stream is ordered after the staging copy and joined before
+    the copy back."""
+    H, dec = dvbs2
+    monkeypatch.setenv("LDPC_IRA_BUDGET_MB", "1")           # 8-codeword chunks: 3 chunks over 2 streams
+    _, x = _llr(H, 21, 1.3, seed=21)
+    r = dec.decode(x, 9, algo="minsum", clamp=20.0, soft="z")
+    ref = oracle.ms_f32(H, x, 9, 20.0)
+    assert np.array_equal(r["bits"], ref["bits"]) and _same(r["soft"], ref["z"])
+    out = ldpc_amd.decode(H, x, 9, algo="minsum", clamp=20.0)
+    assert np.array_equal(np.asarray(out), ref["bits"])
+
+
 def test_not_ira_when_structure_breaks():
     """A DVB-S2 H with one information edge moved is no longer IRA-structured: the generic kernels take it."""
     H, _ = get_code("dvbs2_12")

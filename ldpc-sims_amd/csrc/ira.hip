@@ -99,6 +99,9 @@ __device__ __forceinline__ void rotate_left(float (&c)[D], int rho) {
 // profiles/r05/ab/ab_c4_ira_restructure.txt).  Two tasks side by side per workgroup measured no faster
 // (ab_c4_ira_tpp.txt), nor did several positions per lane (ab_c4_ira_ppl.txt).
 constexpr int kIraLanes = 384;
+#ifndef IRA_DIAG_NOPAR
+#define IRA_DIAG_NOPAR 0  // DIAGNOSTIC BUILD ONLY (wrong results): the VN skips its parity tasks, to price them
+#endif
 
 // app of information variable (g, pos) of degree D: L + its c2v in ascending check order
 template <int D>
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
                 constexpr int D = decltype(DD)::value;
                 if (d == D) ira_vn_info<D>(row, vo, so, pos, L, S, app);
             });
-        } else {
+        } else if (!IRA_DIAG_NOPAR) {
             // parity p_j, j = r + q pos: checks j (its own (r, pos), slot kIPS) and j + 1 (slot kIPS + 1 there)
             const int r = gi - t.G;
             const int p = min(pos, kIZ - 1);

@@ -20,7 +20,8 @@ fi
 if [ $PART = 3 ] || [ $PART = all ]; then
 # one Eb/N0 point (a fixed-count decode does the same work at every point): the PMC passes of the five-point grid
 # (~29 k dispatches) crashed the profiler (SIGSEGV inside the HIP runtime under --pmc, session r5prof)
-LDPC_IRA_STREAMS=1 OUT=$OUT NAME=c4_dvbs2_minsum50 DKERNELS=k_ira_load,k_ira_vn,k_ira_cn,k_ira_out CHUNKS=19 ARGS="--code dvbs2_12 --ebn0 1.5:1:1.5 --batch 4096" bash scripts/gpu_profile.sh || exit 1
+# CHUNKS = ceil(4096 / chunk), chunk = (200 MiB / (8n + 16M bytes)) rounded down to 8 = 200 codewords: 21
+LDPC_IRA_STREAMS=1 OUT=$OUT NAME=c4_dvbs2_minsum50 DKERNELS=k_ira_load,k_ira_vn,k_ira_cn,k_ira_out CHUNKS=21 ARGS="--code dvbs2_12 --ebn0 1.5:1:1.5 --batch 4096" bash scripts/gpu_profile.sh || exit 1
 fi
 if [ $PART = all ]; then
 python3 scripts/counters_combine.py $OUT > $OUT/counters.json && echo "combined -> $OUT/counters.json"

@@ -19,7 +19,7 @@ SEL = {"c1_wifi648_minsum50": ["--kernel", "k_qc_ms_ph", "--last", "11"],
        "c1_wifi648_tanh50": ["--kernel", "k_qc_sp_st", "--last", "11"],
        "c2_wifi1944_tanh50_16qam": ["--kernel", "k_qc_sp_rs", "--last", "11"],
        "c3_wifi1296_q5_20es": ["--kernel", "k_qc_qms_pk", "--last", "11"],
-       "c4_dvbs2_minsum50": ["--decode-kernels", "k_ira_load,k_ira_vn,k_ira_cn,k_ira_out", "--chunks", "19",
+       "c4_dvbs2_minsum50": ["--decode-kernels", "k_ira_load,k_ira_vn,k_ira_cn,k_ira_out", "--chunks", "21",
                              "--last", "1"]}
 
 

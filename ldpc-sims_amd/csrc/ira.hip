@@ -118,6 +118,17 @@ struct ParBuf {
     int64_t stride;
 };
 
+// Early termination (LDPC_F_EARLY_STOP; the oracle's ms_f32: after iteration it the decisions of app_{it+1} are
+// tested, and a codeword whose syndrome is zero stops with iters_used = it + 1).  CN(it), it >= 1, tests app_it —
+// the posteriors it reads anyway — and ORs "some check unsatisfied" into uns[it & 1][cw]; VN(it + 1) reads it: zero
+// means converged at it (conv[cw] = it, nothing more runs for that codeword; its app_it stays in place — the parity
+// part in the buffer of iteration it), otherwise the first workgroup zeroes uns[(it + 1) & 1][cw] for CN(it + 1).
+struct IraEs {
+    int32_t* conv;     // per codeword of the chunk: 0 = running, else iterations used
+    int32_t* uns[2];   // per codeword: some check unsatisfied (uns[0] starts nonzero: nothing tested yet)
+    int it;            // the iteration of this launch
+};
+
 // app of information variable (g, pos) of degree D: L + its c2v in ascending check order
 template <int D>
 __device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int64_t vo, int64_t so, int pos,
@@ -152,14 +163,24 @@ __device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int
 // the 360 positions.  Writes app in the permuted layout (information: g*360 + m, parity: k + a*360 + b).
 // Parity rows: every row (pgrp = 0), or only the last row of each group of pgrp check rows (IRA_CNPAR: the check
 // kernel formed the others); their posteriors go to `par`.
-template <int MAXDV>
+template <int MAXDV, bool ES>
 __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __restrict__ L, float* __restrict__ app,
                                                       const IraState* __restrict__ S, ParBuf par, int pgrp,
-                                                      int Bc, int tpw) {
+                                                      int Bc, int tpw, IraEs es) {
     const int T = t.G + (pgrp > 0 ? (t.q + pgrp - 1) / pgrp : t.q);
     int cw, tb;
     if (!ira_task((T + tpw - 1) / tpw, Bc, cw, tb)) return;
     const int pos = threadIdx.x;
+    if constexpr (ES) {  // (wave-uniform loads)
+        if (es.conv[cw] != 0) return;
+        if (es.it >= 1) {
+            if (es.uns[(es.it - 1) & 1][cw] == 0) {  // app_{it-1} satisfies every check: converged at it - 1
+                if (pos == 0) es.conv[cw] = es.it - 1;
+                return;
+            }
+            if (tb == 0 && pos == 0) es.uns[es.it & 1][cw] = 0;  // CN(it) accumulates here
+        }
+    }
     for (int gi = tb * tpw; gi < T && gi < (tb + 1) * tpw; ++gi) {
         const int64_t so = (int64_t)cw * t.M;
         if (gi < t.G) {
@@ -195,13 +216,17 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
 // and its own state, writes the new state (the oracle's k_cn_ms arithmetic on v2c = app - c2v).
 // Parity posteriors read from `pr`; with FUSE (IRA_CNPAR) the next iteration's parity posteriors of every row but
 // the group's last are written to `pw` (the variable kernel forms the rest), from L (`L`) and the new states.
-template <int MAXR, bool FUSE>
+template <int MAXR, bool FUSE, bool ES>
 __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __restrict__ app, ParBuf pr, ParBuf pw,
                                                       const float* __restrict__ L, IraState* __restrict__ S, int Bc,
-                                                      float clamp, float alpha, float beta, int tpw) {
+                                                      float clamp, float alpha, float beta, int tpw, IraEs es) {
     int cw, tb;
     if (!ira_task((t.q + tpw - 1) / tpw, Bc, cw, tb)) return;
     const int pos = threadIdx.x;
+    if constexpr (ES) {
+        if (es.conv[cw] != 0) return;
+    }
+    bool unsat = false;  // ES, it >= 1: some check of this lane's rows fails on app_it
     const int p = min(pos, kIZ - 1);
     const float* const prc = pr.p + (int64_t)cw * pr.stride;
     IraState prev = {0.0f, 0.0f, 0u};  // FUSE: the new state of the previous row at this position
@@ -227,6 +252,17 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
                 v[s] = app[ao + (int64_t)g * kIZ + m];
             }
         });
+        if constexpr (ES) {  // the check on app_it: xor of its variables' decisions (z = app / 2)
+            if (es.it >= 1) {
+                bool par = Num<float>::bit(0.5f * ap0);
+                if (ra > 0 || p > 0) par ^= Num<float>::bit(0.5f * ap1);
+                static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
+                    constexpr int s = decltype(SS)::value;
+                    if (s < R) par ^= Num<float>::bit(0.5f * v[s]);
+                });
+                unsat |= par && pos < kIZ;
+            }
+        }
         float min1 = __builtin_inff(), min2 = __builtin_inff();
         int idx = -1;
         uint32_t sgn = 0;
@@ -271,6 +307,9 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
             prev = nst;
         }
     }
+    if constexpr (ES) {
+        if (__ballot(unsat) != 0 && (threadIdx.x & 63) == 0) atomicOr(es.uns[es.it & 1] + cw, 1);
+    }
 }
 
 // natural [B][n] llr -> permuted L = -llr: information part as is, parity block [360][q] (index b*q + a)
@@ -302,8 +341,16 @@ __global__ __launch_bounds__(256) void k_ira_load(const float* __restrict__ llr,
 
 // z = 0.5 app (the oracle's final layer for min-sum, bp.py:51's decision rule) back to the natural layout:
 // bits (np.round(p1) rule) and soft (p1 = 1 - sigmoid(z), or z).
-__global__ __launch_bounds__(256) void k_ira_out(const float* __restrict__ app, ParBuf par, uint8_t* __restrict__ bits,
-                                                 float* __restrict__ soft, int soft_z, int n, int k, int q) {
+// ES: a converged codeword's posteriors are those of iteration conv[cw]: its parity part is in par[conv & 1];
+// iters_used (the chunk's slice, or null) gets conv or iters
+__global__ __launch_bounds__(256) void k_ira_out(const float* __restrict__ app, ParBuf p0, ParBuf p1, int iters,
+                                                 const int32_t* __restrict__ conv, int32_t* __restrict__ used,
+                                                 uint8_t* __restrict__ bits, float* __restrict__ soft, int soft_z, int n,
+                                                 int k, int q) {
+    const int32_t cu = conv ? conv[blockIdx.y] : 0;
+    const int u = cu ? cu : iters;
+    const ParBuf par = (u & 1) ? p1 : p0;
+    if (used && blockIdx.x == 0 && threadIdx.x == 0) used[blockIdx.y] = u;
     __shared__ float tile[64][65];
     const int64_t base = (int64_t)blockIdx.y * n;
     const int ninfo = (k + 1023) / 1024;
@@ -430,7 +477,7 @@ void ira_free(IRASpec* s) {
 bool ira_supports(const IRASpec* s, const ldpc_params& p) {
     if (!s) return false;
     if (p.algo != LDPC_ALGO_MIN_SUM) return false;
-    if (p.flags & (LDPC_F_EARLY_STOP | LDPC_F_F64)) return false;
+    if (p.flags & LDPC_F_F64) return false;
     if (getenv("LDPC_NO_IRA")) return false;  // A/B against the generic kernels in one process
     return s->maxdv <= 16 && s->maxr <= kICS;
 }
@@ -464,11 +511,12 @@ static int ira_streams() {
     return v < 1 ? 1 : (v > 4 ? 4 : v);
 }
 
-// L, app, check states and (IRA_CNPAR) the second parity-posterior buffer of bc codewords
+// L, app, check states, (IRA_CNPAR) the second parity-posterior buffer and the early-stop words (conv, uns[2])
+// of bc codewords
 static size_t ira_set_bytes(const IRASpec* s, int64_t bc) {
     auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
     return 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * sizeof(IraState)) +
-           (IRA_CNPAR ? a256((size_t)bc * s->M * 4) : 0);
+           (IRA_CNPAR ? a256((size_t)bc * s->M * 4) : 0) + a256((size_t)bc * 12);
 }
 
 size_t ira_workspace(const IRASpec* s, int64_t B, const ldpc_params&) {
@@ -515,12 +563,19 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
         const ParBuf P1 = IRA_CNPAR ? ParBuf{(float*)(w + 2 * a256((size_t)bc * s->n * 4) +
                                                       a256((size_t)bc * s->M * sizeof(IraState))), s->M}
                                     : P0;
+        int32_t* esw = (int32_t*)(w + 2 * a256((size_t)bc * s->n * 4) + a256((size_t)bc * s->M * sizeof(IraState)) +
+                                  (IRA_CNPAR ? a256((size_t)bc * s->M * 4) : 0));
+        const bool es_on = (p.flags & LDPC_F_EARLY_STOP) != 0;
+        IraEs es{esw, {esw + bc, esw + 2 * bc}, 0};
         const int b = (int)(B - o < bc ? B - o : bc);
         const int64_t vo = o * s->n;
         const unsigned cw8 = (unsigned)((b + 7) / 8) * 8;
         k_ira_load<<<dim3(tiles, b), 256, 0, q>>>(llr + vo, L, s->n, s->k, s->q);
         if (hipMemsetAsync(S, 0, (size_t)b * s->M * sizeof(IraState), q) != hipSuccess)
             return set_error(LDPC_EHIP, "IRA state init failed");
+        if (es_on && (hipMemsetAsync(es.conv, 0, (size_t)b * 4, q) != hipSuccess ||
+                      hipMemsetAsync(es.uns[0], 1, (size_t)b * 4, q) != hipSuccess))  // nonzero: untested
+            return set_error(LDPC_EHIP, "IRA early-stop init failed");
         const unsigned gcn = cw8 * (unsigned)((s->q + tpw - 1) / tpw);
         for (int it = 0; it <= p.iters; ++it) {
             // VN(it) writes the parity rows the check kernel did not form into P[it & 1] (all of them before the
@@ -529,20 +584,29 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
             const int pgrp = (IRA_CNPAR && it > 0) ? tpw : 0;
             const int tv = s->G + (pgrp ? (s->q + pgrp - 1) / pgrp : s->q);
             const unsigned gvn = cw8 * (unsigned)((tv + tpv - 1) / tpv);
-            if (s->maxdv <= 8) k_ira_vn<8><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, pv, pgrp, b, tpv);
-            else k_ira_vn<16><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, pv, pgrp, b, tpv);
+            es.it = it;
+#define IRA_VN(D, E) k_ira_vn<D, E><<<gvn, kIraLanes, 0, q>>>(t, L, app, S, pv, pgrp, b, tpv, es)
+#define IRA_CN(R, E) k_ira_cn<R, IRA_CNPAR, E><<<gcn, kIraLanes, 0, q>>>(t, app, pv, pn, L, S, b, p.clamp, p.alpha, p.beta, tpw, es)
+            if (s->maxdv <= 8) {
+                if (es_on) IRA_VN(8, true); else IRA_VN(8, false);
+            } else {
+                if (es_on) IRA_VN(16, true); else IRA_VN(16, false);
+            }
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
-            if (s->maxr <= 8)
-                k_ira_cn<8, IRA_CNPAR><<<gcn, kIraLanes, 0, q>>>(t, app, pv, pn, L, S, b, p.clamp, p.alpha, p.beta, tpw);
-            else
-                k_ira_cn<kICS, IRA_CNPAR><<<gcn, kIraLanes, 0, q>>>(t, app, pv, pn, L, S, b, p.clamp, p.alpha, p.beta, tpw);
+            if (s->maxr <= 8) {
+                if (es_on) IRA_CN(8, true); else IRA_CN(8, false);
+            } else {
+                if (es_on) IRA_CN(kICS, true); else IRA_CN(kICS, false);
+            }
+#undef IRA_VN
+#undef IRA_CN
         }
-        k_ira_out<<<dim3(tiles, b), 256, 0, q>>>(app, (p.iters & 1) ? P1 : P0, bits ? bits + vo : nullptr,
+        k_ira_out<<<dim3(tiles, b), 256, 0, q>>>(app, P0, P1, p.iters, es_on ? es.conv : nullptr,
+                                                 iters_used ? iters_used + o : nullptr, bits ? bits + vo : nullptr,
                                                  soft ? soft + vo : nullptr, soft_z, s->n, s->k, s->q);
     }
     if (nf > 0)
         if (const int rc = aux_join(st, nf)) return rc;
-    if (iters_used) fill_i32(iters_used, B, p.iters, st);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(LDPC_EHIP, "IRA kernel launch: %s", hipGetErrorString(e));
     return LDPC_OK;

@@ -49,7 +49,7 @@ def test_kernel_path_selection(dvbs2):
     assert dec.kernel_path(dec.params(50, "minsum", 20.0, alpha=0.75, beta=0.5)) == "ira-z360"
     # not (yet) covered by the IRA kernels: the generic CSR kernels take them
     assert dec.kernel_path(dec.params(50, "minsum", 20.0, force_generic=True)) == "generic-csr"
-    assert dec.kernel_path(dec.params(50, "minsum", 20.0, early_stop=True)) == "generic-csr"
+    assert dec.kernel_path(dec.params(50, "minsum", 20.0, early_stop=True)) == "ira-z360"
     assert dec.kernel_path(dec.params(50, "tanh", 20.0)) == "generic-csr"
     wifi = ldpc_amd.get_decoder(get_code("wifi648_12")[0])
     assert wifi.kernel_path(wifi.params(50, "minsum", 20.0)) == "qc-z27"
@@ -138,6 +138,25 @@ def test_shaped_code_and_host_pointers():
     ref = oracle.ms_f32(H, x, 30, 20.0)
     assert np.array_equal(r["bits"], ref["bits"]) and np.array_equal(r["bits"], g["bits"])
     assert _same(r["soft"], g["soft"])
+
+
+@pytest.mark.parametrize("ebn0,budget", [(1.0, None), (1.4, "1"), (1.8, None), (2.5, "3")])
+def test_early_stop_vs_oracle_bitwise(dvbs2, ebn0, budget, monkeypatch):
+    """Early termination (the oracle's ms_f32 early_stop: app_{it+1} tested after each iteration): bits, z and
+    iters_used bit for bit against the oracle and the generic kernels, from the waterfall (few converge) to where
+    every codeword stops early, over one chunk and over several chunks on two streams."""
+    H, dec = dvbs2
+    if budget is not None:
+        monkeypatch.setenv("LDPC_IRA_BUDGET_MB", budget)
+    _, x = _llr(H, 19, ebn0, seed=int(ebn0 * 100))
+    bits, z, used = _decode(dec, x, 30, clamp=20.0, early_stop=True)
+    ref = oracle.ms_f32(H, x, 30, 20.0, early_stop=True)
+    assert np.array_equal(used, ref["iters_used"]), (used, ref["iters_used"])
+    assert np.array_equal(bits, ref["bits"]) and _same(z, ref["z"])
+    gb, gz, gu = _decode(dec, x, 30, clamp=20.0, early_stop=True, force_generic=True)
+    assert np.array_equal(gu, used) and np.array_equal(gb, bits) and _same(gz, z)
+    if ebn0 >= 1.8:
+        assert (used < 30).all()
 
 
 def test_host_pointers_with_forked_chunks(dvbs2, monkeypatch):

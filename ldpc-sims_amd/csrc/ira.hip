@@ -23,8 +23,9 @@
 // Bytes per codeword-iteration beyond L2 (each codeword's tasks run on one XCD back to back, so the
 // re-reads of its check states and posteriors hit L2): L (4n) + states (12M) + app (4n) in the VN, app (4n)
 // + states read and written (24M) in the CN = 16n + 36M = 2.1 MB for DVB-S2 1/2, against 3.89 MB for the
-// two-array dataflow.  A chunk of codewords whose arrays (8n + 12M bytes each) fit the Infinity Cache
-// decodes all its iterations before the next chunk starts.
+// two-array dataflow.  A chunk of codewords whose arrays (8n + 16M bytes each) fit the Infinity Cache decodes
+// all its iterations before the next chunk starts; chunks go round-robin over two streams.  Also here: the parity
+// posteriors formed by the check kernel (IRA_CNPAR) and early termination (IraEs) — DESIGN.md §3.8.
 #include <stdlib.h>
 
 #include <algorithm>
@@ -50,7 +51,6 @@ struct IRADev {
     int q, G, k, n, M;
 };
 
-// c2v of slot `slot` from a check state: the argmin slot gets mag2, every other mag1; sign bit from meta
 // One check's state, 12 bytes read and written as one dwordx3: the two output magnitudes and the meta word
 struct IraState {
     float m1, m2;
@@ -60,6 +60,7 @@ static_assert(sizeof(IraState) == 12, "one dwordx3 per check state");
 
 __device__ __forceinline__ IraState ira_ld(const IraState* __restrict__ p) { return *p; }
 
+// c2v of slot `slot` from a check state: the argmin slot gets mag2, every other mag1; sign bit from meta
 __device__ __forceinline__ float ira_c2v(const IraState& st, int slot) {
     const float mag = ((st.meta >> 27) == (uint32_t)slot) ? st.m2 : st.m1;
     return u2f(f2u(mag) | ((st.meta << (31 - slot)) & 0x80000000u));

@@ -173,6 +173,43 @@ def test_host_pointers_with_forked_chunks(dvbs2, monkeypatch):
     assert np.array_equal(np.asarray(out), ref["bits"])
 
 
+def _shaped_ira(q, G, degs, seed, Z=360):
+    """A random IRA code with the DVB-S2 structure: G groups of Z information bits (row degrees `degs`), q rows
+    of checks per position; every residue mod q gets the same number of addresses, distinct inside a row."""
+    from ldpc_amd.codes import _ira_code
+    rng = np.random.default_rng(seed)
+    per = sum(degs) // q
+    assert per * q == sum(degs)
+    left, rows = np.full(q, per), []
+    for d in degs:                                        # the d residues with the most addresses left (random ties)
+        perm = rng.permutation(q)
+        r = perm[np.argsort(-left[perm], kind="stable")[:d]]
+        left[r] -= 1
+        rows.append(r)
+    assert (left == 0).all()
+    groups = [r + q * rng.integers(0, Z, size=len(r)) for r in rows]
+    k, m = G * Z, q * Z
+    return _ira_code(groups, f"ira_q{q}_g{G}", n=k + m, k=k, q=q, Z=Z)
+
+
+@pytest.mark.parametrize("shape", ["r23_long", "short"])
+def test_other_ira_shapes_vs_oracle(shape):
+    """Other IRA shapes through the same kernels: a rate-2/3-shaped normal frame (q = 60, 12 groups of degree 13 —
+    the 16-slot variable kernel — and 108 of degree 3) and a short one (q = 25, 20 groups): bits, z and iteration
+    counts bitwise against the oracle, fixed count and early stop."""
+    if shape == "r23_long":                                 # _llr's noise is set for rate 1/2: points shifted
+        H, pts = _shaped_ira(60, 120, [13] * 12 + [3] * 108, seed=23), ((3.2, False), (4.0, True))
+    else:
+        H, pts = _shaped_ira(25, 20, [8] * 8 + [3] * 12, seed=7), ((1.0, False), (2.6, True))
+    dec = ldpc_amd.get_decoder(H)
+    assert dec.kernel_path(dec.params(20, "minsum", 20.0)) == "ira-z360"
+    for ebn0, es in pts:
+        _, x = _llr(H, 11, ebn0, seed=31)
+        bits, z, used = _decode(dec, x, 20, clamp=20.0, early_stop=es)
+        ref = oracle.ms_f32(H, x, 20, 20.0, early_stop=es)
+        assert np.array_equal(used, ref["iters_used"]) and np.array_equal(bits, ref["bits"]) and _same(z, ref["z"]), (ebn0, es)
+
+
 def test_not_ira_when_structure_breaks():
     """A DVB-S2 H with one information edge moved is no longer IRA-structured: the generic kernels take it."""
     H, _ = get_code("dvbs2_12")

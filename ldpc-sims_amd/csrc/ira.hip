@@ -109,6 +109,9 @@ constexpr int kIraLanes = 384;
 // check workgroup's group (their r + 1 lives in another workgroup) — 15 of 90 for DVB-S2 1/2 at 6 rows per group.
 // The posteriors it writes are the NEXT iteration's, while other check workgroups still read this iteration's: the
 // parity posteriors ping-pong between two buffers (ParBuf), M floats per codeword more.  Bitwise the same.
+#ifndef IRA_DIAG_VN4
+#define IRA_DIAG_VN4 0  // DIAGNOSTIC BUILD ONLY (wrong results): information c2v read as 4 contiguous bytes, to price 12 -> 4
+#endif
 #ifndef IRA_CNPAR
 #define IRA_CNPAR 1
 #endif
@@ -151,7 +154,12 @@ __device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int
         b -= w ? kIZ : 0;
         wrapped += w;
         const int64_t i = so + (int64_t)ra * kIZ + b;
+#if IRA_DIAG_VN4
+        const float x = reinterpret_cast<const float*>(S)[i];
+        c[t] = ira_c2v(IraState{x, x, (uint32_t)slot << 27}, slot);
+#else
         c[t] = ira_c2v(ira_ld(S + i), slot);
+#endif
     });
     // entries are sorted by x = a + q s, i.e. by s: the wrapped ones are the last `wrapped` entries and their
     // checks come first in ascending order

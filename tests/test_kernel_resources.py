@@ -11,8 +11,9 @@ waves / units whose LLRs hold an exact zero (erasures, quantized LLRs), which ma
     [2] (1944,5/6) tanh-SP, 16-QAM OFDM   k_qc_sp_rs<Wifi1944_56, 1> (fixed count), k_qc_sp_sl<Wifi1944_56, *, 1>
                                           (early stop; the fixed-count sliced kernel remains for QC_SL_SP_RS=0)
     [3] (1296,2/3) 5-bit min-sum 20 it ES k_qc_qms_pk<Wifi1296_23, *, *>  (packed fp16, two codewords per lane)
-    [4] DVB-S2 64800 rate 1/2, 50 it      generic CSR kernels at degree bound 8 (k_vn_ms/k_cn_ms, k_vn_sp/k_cn_sp),
-                                          k_load_llr, k_final
+    [4] DVB-S2 64800 rate 1/2, 50 it      IRA kernels (ira.hip: k_ira_vn<8, *>, k_ira_cn<8, true, *>, k_ira_load,
+                                          k_ira_out); the generic CSR kernels at degree bound 8 (k_vn_ms/k_cn_ms,
+                                          k_vn_sp/k_cn_sp, k_load_llr, k_final) for any other H and for tanh-SP
     drop-in decode_bits on (648,1/2)      k_qc_sp_st<Wifi648_12, false, 1>
 """
 import os
@@ -36,6 +37,10 @@ BASELINE_KERNELS = [
     r"k_load_llr<float>",
     r"k_final<float, 32, (true|false)>",
     r"k_qc_sp_st<ldpc::Wifi648_12, false, 1>",
+    r"k_ira_vn<(8|16), (true|false)>",
+    r"k_ira_cn<(8|24), true, (true|false)>",
+    r"k_ira_load\(",
+    r"k_ira_out\(",
 ]
 MAX_SPILL_OUTSIDE_LOOP = {r"k_qc_sp_rs<ldpc::Wifi1944_56, 1>": 0}
 MAX_SCRATCH_IN_LOOP = 0

@@ -173,6 +173,19 @@ def test_host_pointers_with_forked_chunks(dvbs2, monkeypatch):
     assert np.array_equal(np.asarray(out), ref["bits"])
 
 
+def test_one_codeword_and_empty_batch(dvbs2):
+    """Batch edges on the IRA path: one codeword (a single XCD group slot, one chunk) bitwise against the oracle
+    with and without early stop; an empty batch returns empty outputs without a launch."""
+    H, dec = dvbs2
+    _, x = _llr(H, 1, 1.6, seed=1)
+    for es in (False, True):
+        bits, z, used = _decode(dec, x, 12, clamp=20.0, early_stop=es)
+        ref = oracle.ms_f32(H, x, 12, 20.0, early_stop=es)
+        assert np.array_equal(used, ref["iters_used"]) and np.array_equal(bits, ref["bits"]) and _same(z, ref["z"])
+    r = dec.decode(np.zeros((0, H.n), np.float32), 12, algo="minsum", clamp=20.0, soft="z")
+    assert r["bits"].shape == (0, H.n) and r["soft"].shape == (0, H.n)
+
+
 def _shaped_ira(q, G, degs, seed, Z=360):
     """A random IRA code with the DVB-S2 structure: G groups of Z information bits (row degrees `degs`), q rows
     of checks per position; every residue mod q gets the same number of addresses, distinct inside a row."""

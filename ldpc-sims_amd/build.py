@@ -3,6 +3,7 @@
 Each source compiles to its own object (in parallel), then one link; per-file flags below.
 """
 import os
+import re
 import subprocess
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -35,6 +36,13 @@ PER_FILE = {"qc.hip": ["-fno-honor-nans", *SCHED], "qc_sl.hip": ["-fno-honor-nan
             "qc_pk.hip": ["-fno-honor-nans"], "qc_sl_es.hip": ["-fno-honor-nans"], "qc_es.hip": ["-fno-honor-nans"]}  # iterative-ilp crashes the register allocator on qc_pk (ROCm 7.2)
 
 
+def _hip_includes(src):
+    """The csrc/*.hip files `src` #includes (one level: the per-variant translation units)."""
+    with open(src) as f:
+        names = re.findall(r'^\s*#\s*include\s+"([^"]+\.hip)"', f.read(), re.M)
+    return [os.path.join(os.path.dirname(src), n) for n in names]
+
+
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=(), per_file=True, qc_flags=None) -> str:
     srcs = [os.path.join(HERE, "csrc", s) for (s, _, _) in SRCS]
     deps = srcs + [os.path.join(HERE, "csrc", "common.h"), os.path.join(ROOT, "include", "ldpc_abi.h")]
@@ -54,9 +62,10 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         src = os.path.join(HERE, "csrc", name)
         obj = os.path.join(objdir, oname)
         objs.append(obj)
-        # an object is reused when newer than its source, every header and this script (same flags)
+        # an object is reused when newer than its source, the .hip files it includes (qc_es.hip is qc.hip
+        # built again with other flags), every header and this script (same flags)
         if (not force and not defines and os.path.exists(out) and os.path.exists(obj)
-                and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in [src, *hdrs])):
+                and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in [src, *_hip_includes(src), *hdrs])):
             continue
         cmds.append([*common, *extra, *(PER_FILE.get(name, []) if per_file else []), "-c", "-o", obj, src])
     link = ["hipcc", "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out, *objs]

@@ -96,8 +96,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_WAVES_PER_SIMD_EARLY : QC_WAVES_PER
         constexpr int j = decltype(jj)::value;
         float x = llr[vidx(z, j, C::PHI[j])] * vmask;
         if (QUANT) x = fminf(fmaxf(rintf(x * qinv), -qmax), qmax);
-        app[j] = -x;  // APP before iteration 0 = L + sum(c2v = 0)
+        app[j] = -x;  // L
         if (z < Z) Ls[lbase + j * Z] = app[j];
+        app[j] = app[j] + 0.0f;  // APP before iteration 0 = L + sum(c2v = +0): an L of -0 gives +0 (oracle ms_f32_one)
     });
     if (QUANT) {
 #pragma unroll
@@ -368,8 +369,9 @@ __global__ __launch_bounds__(256, EARLY ? QC_ST_WAVES_PER_SIMD_EARLY : QC_ST_WAV
         constexpr int j = decltype(jj)::value;
         float x = llr[vidx(z, j, C::PHI[j])] * vmask;
         if (QUANT) x = fminf(fmaxf(rintf(x * qinv), -qmax), qmax);
-        app[j] = -x;
+        app[j] = -x;  // L
         if (QC_L128 || z < Z) LS_AT(lrow, j) = app[j];
+        app[j] = app[j] + 0.0f;  // APP_0 = L + sum(c2v = +0): -0 -> +0, as the oracle
     });
     if (QUANT) {
 #pragma unroll
@@ -743,7 +745,7 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
             constexpr int r = decltype(rr)::value;
             static_for<0, C::DEG[r]>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
-                float x = L[C::COL[r][t]] - 0.0f;  // v2c = APP_0 - c2v(= +0), as k_qc_ms_st
+                float x = L[C::COL[r][t]] + 0.0f;  // v2c = APP_0 - c2v(= +0), APP_0 = L + (+0): -0 -> +0
                 if constexpr (QUANT) x = fminf(fmaxf(x, -qmax), qmax);
                 msg[edge_off<C>(r) + t] = x;
             });
@@ -1072,7 +1074,8 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
         constexpr int j = lcol<C>(p);
         float a;
         if (iters > 0 && !early_exit) a = vn_col(pp);
-        else a = Ls[lrow + p];  // iters == 0: APP_0 = L (QUANT: clamped below); early exit: parked APP
+        else a = Ls[lrow + p] + (iters == 0 ? 0.0f : -0.0f);  // iters == 0: APP_0 = L + (+0) (QUANT: clamped
+                                                               // below); early exit: parked APP (x + -0 == x)
         if (QUANT && iters == 0) a = fminf(fmaxf(a, -app_max), app_max);
         if (parked) a = Ls[lrow + p];
         if (ok) {

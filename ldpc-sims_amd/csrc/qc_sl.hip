@@ -51,7 +51,7 @@ void k_qc_ms_sl(const float* __restrict__ llr, int64_t B, int iters, float clamp
             float x = valid ? llr[base + j * Z + t] : 0.0f;
             if (QUANT) x = fminf(fmaxf(rintf(x * qinv), -qmax), qmax);
             Lr[j] = -x;
-            app[j] = QUANT ? fminf(fmaxf(-x, -app_max), app_max) : -x;
+            app[j] = QUANT ? fminf(fmaxf(-x, -app_max), app_max) : -x + 0.0f;  // APP_0 = L + (+0) c2v: -0 -> +0
         });
     }
     float msg[NE];  // c2v of every edge, check frame

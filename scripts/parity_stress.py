@@ -1,0 +1,195 @@
+"""Randomised parity sweep on the GPU, time-budgeted: random code, algorithm, parameters, iteration count, batch
+size, Eb/N0, erasures and LLR scale per trial, each decoded through the product path and compared with the checker
+— bit for bit:
+  min-sum           bits, z and iterations used vs oracle.ms_f32 (oracle/ldpc_oracle.c)
+  5-bit min-sum     bits, z = app / 2 (by value: the integer posteriors' zero has no sign) and iterations used
+                    vs oracle.qms
+  tanh-SP           bits and iterations used bit for bit vs the generic CSR kernels (the QC kernels' arithmetic
+                    is the generic path's, operation for operation), z bit for bit too except on codewords where the
+                    decode meets an edge with a == exp(-|s|) == 1 at a nonzero s (|s| below ~1e-7): the plain
+                    register kernels (fixed count, and the sliced early-stop kernel) apply the a == 1 rule only on
+                    units whose LLRs hold an exact zero
+                    (DESIGN.md §3.5), so there z may differ by a few ulps — counted as "ulp" trials, held to 1e-6
+                    relative, not mismatches.  Soft parity against the reference is the tolerance tests' business
+                    (tests/test_gpu_soft_parity.py, tests/test_gpu_config2.py)
+A test-infrastructure script (the oracle is the checker here, never the thing measured).  Prints one line per
+kernel path and writes a JSON summary; a mismatching trial's inputs go to OUT/stress_fail_<n>.npz.
+
+    python scripts/parity_stress.py --seconds 420 --out gpurun_out/stress
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "ldpc-sims_amd"), os.path.join(ROOT, "oracle")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+import ldpc_amd  # noqa: E402
+import oracle  # noqa: E402
+from ldpc_amd.codes import Encoder, IRAEncoder, get_code  # noqa: E402
+
+CODES = ["wifi648_12", "wifi648_23", "wifi648_34", "wifi648_56", "wifi1296_12", "wifi1296_23", "wifi1296_34",
+         "wifi1296_56", "wifi1944_12", "wifi1944_23", "wifi1944_34", "wifi1944_56", "peg64_32", "dvbs2_12", "dvbs2s_12"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=420.0)
+    ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stress"))
+    ap.add_argument("--only", default="", help="comma-separated trial numbers: replay just these (same seed), each "
+                    "decoded 3 times, to tell a deterministic mismatch from a nondeterministic one")
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    rng = np.random.default_rng(a.seed)
+    have = set(ldpc_amd.codes.available_codes())
+    codes = [c for c in CODES if c in have]
+    cache = {}
+
+    def code(name):
+        if name not in cache:
+            H, _ = get_code(name)
+            enc = IRAEncoder(H) if name.startswith("dvbs2") else Encoder(H)
+            cache[name] = (H, enc)
+        return cache[name]
+
+    decs = {}
+
+    def decoder(name, H):
+        if name not in decs:
+            decs[name] = ldpc_amd.get_decoder(H)
+        return decs[name]
+
+    only = {int(t) for t in a.only.split(",") if t}
+    stats, fails, t0, trial = {}, [], time.time(), 0
+    last = t0
+    while (time.time() - t0 < a.seconds) if not only else (trial < max(only)):
+        trial += 1
+        name = codes[rng.integers(len(codes))]
+        H, enc = code(name)
+        big = name.startswith("dvbs2")
+        algos = ("minsum", "qminsum", "tanh") if name.startswith("wifi") else ("minsum", "tanh")  # 5-bit: QC only
+        algo = "minsum" if big else algos[rng.integers(len(algos))]
+        B = int(rng.integers(1, 13 if big else 300))
+        iters = int(rng.integers(0, 21 if big else 51))
+        es = bool(rng.integers(2))
+        ebn0 = float(rng.uniform(-1.0, 6.0))
+        cw = enc.encode(rng.integers(0, 2, size=(B, enc.k)))
+        sigma = np.sqrt(1.0 / (2 * 0.5 * 10 ** (ebn0 / 10)))
+        x = (-2.0 * ((1.0 - 2.0 * cw) + sigma * rng.standard_normal(cw.shape)) / sigma**2).astype(np.float32)
+        if rng.random() < 0.2:
+            x[rng.random(x.shape) < 0.05] = 0.0                   # erasures
+        if rng.random() < 0.1:
+            x *= np.float32(10.0 ** rng.uniform(-3, 6))           # LLR scale extremes
+        if only and trial not in only:       # replay: the same draws as the recorded run, no GPU work
+            if algo == "minsum":
+                rng.choice([6.0, 20.0, 100.0]), rng.choice([1.0, 0.75, 0.8125]), rng.choice([0.0, 0.0, 0.5])
+            elif algo == "qminsum":
+                rng.choice([0.5, 1.0, 2.0]), rng.choice([0, 0, 1])
+            else:
+                rng.choice([10.0, 20.0])
+            continue
+        desc = dict(trial=trial, code=name, algo=algo, B=B, iters=iters, early_stop=es, ebn0=round(ebn0, 3))
+        if only:
+            print("replay", json.dumps(desc), flush=True)
+        dec = decoder(name, H)
+        xg = torch.from_numpy(x).cuda()
+        if algo == "minsum":
+            clamp = float(rng.choice([6.0, 20.0, 100.0]))
+            alpha = float(rng.choice([1.0, 0.75, 0.8125]))
+            beta = float(rng.choice([0.0, 0.0, 0.5]))
+            desc.update(clamp=clamp, alpha=alpha, beta=beta)
+            p = dec.params(iters, "minsum", clamp, alpha=alpha, beta=beta, early_stop=es)
+            r = dec.decode(xg, iters, algo="minsum", clamp=clamp, alpha=alpha, beta=beta, early_stop=es, soft="z",
+                           want_iters=True)
+            ref = oracle.ms_f32(H, x, iters, clamp, alpha, beta, early_stop=es)
+            want = (ref["bits"], ref["z"], ref["iters_used"])
+        elif algo == "qminsum":
+            qstep = float(rng.choice([0.5, 1.0, 2.0]))
+            beta = int(rng.choice([0, 0, 1]))
+            desc.update(qstep=qstep, beta=beta)
+            p = dec.params(iters, "qminsum", 20.0, beta=float(beta), early_stop=es)
+            r = dec.decode(xg, iters, algo="qminsum", qstep=qstep, beta=float(beta), early_stop=es, soft="z",
+                           want_iters=True)
+            q = np.clip(np.rint(x * (np.float32(1.0) / np.float32(qstep))), -15, 15).astype(np.int8)
+            ref = oracle.qms(H, q, iters, 15, 127, beta, early_stop=es)
+            want = (ref["bits"], (0.5 * ref["app"]).astype(np.float32), ref["iters_used"])
+        else:
+            clamp = float(rng.choice([10.0, 20.0]))
+            desc.update(clamp=clamp, zeros=int((x == 0).sum()), maxabs=float(np.abs(x).max()))
+            if only:                          # determinism: three decodes of each path
+                outs = {}
+                for fg in (False, True):
+                    zs = []
+                    for _ in range(3):
+                        o = dec.decode(xg, iters, algo="tanh", clamp=clamp, early_stop=es, soft="z", force_generic=fg)
+                        torch.cuda.synchronize()
+                        zs.append(o["soft"].cpu().numpy().view(np.uint32))
+                    outs[fg] = zs
+                    print(trial, "generic" if fg else "qc", "repeat diffs", [int((zs[0] != zz).sum()) for zz in zs[1:]],
+                          flush=True)
+                d = outs[False][0] != outs[True][0]
+                rows = np.nonzero(d.any(1))[0][:10]
+                za, zb = outs[False][0].view(np.float32), outs[True][0].view(np.float32)
+                rel = [float(np.max(np.abs(za[k] - zb[k]) / np.maximum(np.abs(zb[k]), 1.0))) for k in rows]
+                bb = dec.decode(xg, iters, algo="tanh", clamp=clamp, early_stop=es, force_generic=True)["bits"]
+                ok_rows = [bool((bb[k].cpu().numpy() == cw[k]).all()) for k in rows]
+                print(trial, "qc vs generic", int(d.sum()), "rows", rows.tolist(), "zeros in those rows",
+                      [int((x[k] == 0).sum()) for k in rows], "max rel dz", rel, "decoded", ok_rows, flush=True)
+            p = dec.params(iters, "tanh", clamp, early_stop=es)
+            r = dec.decode(xg, iters, algo="tanh", clamp=clamp, early_stop=es, soft="z", want_iters=True)
+            g = dec.decode(xg, iters, algo="tanh", clamp=clamp, early_stop=es, soft="z", want_iters=True,
+                           force_generic=True)
+            torch.cuda.synchronize()
+            want = (g["bits"].cpu().numpy(), g["soft"].cpu().numpy(), g["iters_used"].cpu().numpy())
+        torch.cuda.synchronize()
+        path = dec.kernel_path(p) + ("/es" if es else "")
+        got = (r["bits"].cpu().numpy(), r["soft"].cpu().numpy(), r["iters_used"].cpu().numpy())
+        # z bit for bit; the 5-bit decoder's posteriors are integers, whose zero has no sign: compared by value
+        zv = (lambda u: u) if algo == "qminsum" else (lambda u: u.view(np.uint32))
+        zsame = np.array_equal(zv(got[1]), zv(want[1]))
+        ulp = False
+        if not zsame and algo == "tanh":  # the plain kernels' a == 1 case (see the docstring)
+            rel = np.abs(got[1] - want[1]) / np.maximum(np.abs(want[1]), 1.0)
+            ulp = zsame = bool(rel.max() <= 1e-6)
+        ok = np.array_equal(got[0], want[0]) and zsame and np.array_equal(got[2], want[2])
+        key = f"{name} {algo} {path}"
+        s = stats.setdefault(key, [0, 0, 0, 0])
+        s[0] += 1
+        s[1] += B
+        s[3] += ulp
+        if not ok:
+            s[2] += 1
+            desc.update(path=path, bits_diff=int((got[0] != want[0]).sum()),
+                        z_diff=int((zv(got[1]) != zv(want[1])).sum()),
+                        iters_diff=int((got[2] != want[2]).sum()))
+            fails.append(desc)
+            if len(fails) <= 5:
+                np.savez_compressed(os.path.join(a.out, f"stress_fail_{len(fails)}.npz"), llr=x,
+                                    desc=json.dumps(desc))
+            print("MISMATCH", json.dumps(desc), flush=True)
+        if time.time() - last > 30:
+            last = time.time()
+            print(f"{last - t0:.0f} s: {trial} trials, {len(fails)} mismatches", flush=True)
+    for k in sorted(stats):
+        print(f"{k:48s} trials {stats[k][0]:4d} codewords {stats[k][1]:6d} mismatches {stats[k][2]}"
+              + (f"  (ulp-level z: {stats[k][3]})" if stats[k][3] else ""))
+    summary = dict(seconds=round(time.time() - t0, 1), seed=a.seed, trials=trial, mismatches=len(fails),
+                   per_path={k: dict(trials=v[0], codewords=v[1], mismatches=v[2], ulp_z_trials=v[3])
+                             for k, v in stats.items()},
+                   failures=fails[:20])
+    with open(os.path.join(a.out, "summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(f"{trial} trials, {len(fails)} mismatches")
+    return 1 if fails else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

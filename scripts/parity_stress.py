@@ -41,16 +41,17 @@ CODES = ["wifi648_12", "wifi648_23", "wifi648_34", "wifi648_56", "wifi1296_12", 
          "wifi1296_56", "wifi1944_12", "wifi1944_23", "wifi1944_34", "wifi1944_56", "peg64_32", "dvbs2_12", "dvbs2s_12"]
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=420.0)
+    ap.add_argument("--trials", type=int, default=0, help="stop after this many trials (0: time budget only)")
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stress"))
     ap.add_argument("--extended", action="store_true", help="also fp64 tanh-SP vs oracle.sp_f64 (1e-8 relative) "
                     "and host (numpy) inputs through the library's staging path")
     ap.add_argument("--only", default="", help="comma-separated trial numbers: replay just these (same seed), each "
                     "decoded 3 times, to tell a deterministic mismatch from a nondeterministic one")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     os.makedirs(a.out, exist_ok=True)
     rng = np.random.default_rng(a.seed)
     have = set(ldpc_amd.codes.available_codes())
@@ -74,7 +75,8 @@ def main():
     only = {int(t) for t in a.only.split(",") if t}
     stats, fails, t0, trial = {}, [], time.time(), 0
     last = t0
-    while (time.time() - t0 < a.seconds) if not only else (trial < max(only)):
+    while ((time.time() - t0 < a.seconds and (not a.trials or trial < a.trials)) if not only
+           else (trial < max(only))):
         trial += 1
         name = codes[rng.integers(len(codes))]
         H, enc = code(name)

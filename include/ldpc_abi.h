@@ -16,6 +16,11 @@
 extern "C" {
 #endif
 
+/* ABI revision of this header.  2: ldpc_decode gained iters_used (before the stream argument) in round 5 —
+ * a caller built against revision 1 would pass its stream where iters_used is read.  Loaders compare
+ * ldpc_abi_version() with the revision they were written for and refuse a mismatch (ldpc_amd/_abi.py does). */
+#define LDPC_ABI_VERSION 2
+
 typedef struct ldpc_graph ldpc_graph;
 
 enum {
@@ -74,7 +79,8 @@ int ldpc_graph_destroy(ldpc_graph* g);
 int ldpc_graph_info(const ldpc_graph* g, int32_t* m, int32_t* n, int32_t* nnz, int32_t* qc_z);
 
 /* The kernel family a decode with these params runs on this graph: "qc-z<Z>" (register-resident
- * quasi-cyclic kernels, 802.11n), "ira-z360" (DVB-S2-structured IRA codes, min-sum, fixed iterations) or
+ * quasi-cyclic kernels, 802.11n), "ira-z360" (DVB-S2-structured IRA codes, min-sum, fixed count or early
+ * stop) or
  * "generic-csr" (any H).  Introspection only (benchmarks label their records with it); NULL on bad
  * arguments.  The string is thread-local and valid until the next call on this thread.  No reference
  * counterpart: the reference has one code path (dense masks, bp/masking.py). */
@@ -195,6 +201,8 @@ int ldpc_adc_quantize(const float* rx, int64_t nsym, int32_t num_bits, double cl
 const char* ldpc_last_error(void);
 int ldpc_device_count(void);
 const char* ldpc_version(void);
+/* LDPC_ABI_VERSION of the header the library was built from (compare before binding any other symbol). */
+int ldpc_abi_version(void);
 
 #ifdef __cplusplus
 }

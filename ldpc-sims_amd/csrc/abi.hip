@@ -316,7 +316,9 @@ extern "C" {
 
 const char* ldpc_last_error(void) { return g_err.c_str(); }
 
-const char* ldpc_version(void) { return "ldpc-mi355x 0.1 (gfx950)"; }
+const char* ldpc_version(void) { return "ldpc-mi355x 0.2 (gfx950)"; }
+
+int ldpc_abi_version(void) { return LDPC_ABI_VERSION; }
 
 int ldpc_device_count(void) {
     int c = 0;

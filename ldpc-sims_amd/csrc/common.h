@@ -270,10 +270,13 @@ __device__ __forceinline__ void ds_tie(DSet& pre, float (&g)[d]) {
 // rounded through v_rcp_f32, and several such edges per check (erasures, quantized LLRs) add up to a flipped
 // hard decision (tests/golden/bp_zeros.npz).  cn_ds_row<..., FIX = true> marks the row's a == 1 edges in the low
 // bits of the row's sign word (whose bit 31 alone the outputs read, so no register is added) and resets each
-// output whose other edges include one to its sign bit as it is formed.  The register kernels run their whole
-// iteration loop in that form for a wave (or unit) whose LLRs hold an exact zero — the source of a == 1 edges:
-// s = 0 needs L = 0 or an exact cancellation — and in the plain form otherwise, so the common path keeps its
-// registers and schedule; the generic kernels apply the rule always.
+// output whose other edges include one to its sign bit as it is formed.
+// THE RULE (round 6, one for every kernel and the oracle): it applies to the codewords whose LLRs hold an exact
+// zero (+-0) — the source of a == 1 edges: s = 0 needs L = 0 or an exact cancellation — for all their
+// iterations; a codeword without one runs the plain form throughout, where an a == 1 edge (an exact
+// cancellation, or |s| so small that exp rounds to 1) leaves its partners within 2^-23 (log2 units) of 0.  The
+// register kernels run the FIX loop for a wave / unit with such a codeword (fixm masks the lanes of its other
+// codeword), the plain loop otherwise; the generic kernels read a flag per codeword (k_load_llr).
 #ifndef QC_SP_FIXZ
 #define QC_SP_FIXZ 1  // register kernels: the FIX loop for waves / units with an exact-zero LLR (0: never)
 #endif
@@ -293,8 +296,10 @@ __device__ __forceinline__ float ds_fix_one(float y, uint32_t sgw) {
     return (sgw & 0x7fffffffu & ~(1u << t)) ? u2f(f2u(y) & 0x80000000u) : y;
 }
 
+// fixm (FIX): 0x7fffffff where the lane's codeword holds an exact-zero LLR, 0 where it does not (the rule is per
+// codeword: a lane of a codeword without one keeps the plain outputs, whatever its unit's other codeword has)
 template <int d, int SERIAL, int LAG = 0, int BLOCK = DS_BLOCK, bool FIX = false>
-__device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
+__device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2, uint32_t fixm = 0x7fffffffu) {
     const float clamp = cmax2;  // (log2 units, sp_cmax2)
     constexpr auto tie_after = [](int t) { return SERIAL > 0 && (t + 1) % SERIAL == 0; };
 
@@ -305,7 +310,7 @@ __device__ __forceinline__ void cn_ds_row(float (&g)[d], float cmax2) {
         sg = __builtin_amdgcn_bitop3_b32(sg, f2u(g[k]), f2u(g[k + 1]), 0x96);
     });
     if constexpr (d % 2 == 0) sg ^= f2u(g[d - 1]);
-    if constexpr (FIX && d > 1) sg = (sg & 0x80000000u) | ds_ones(g);  // the row's a == 1 edges (ds_fix_one)
+    if constexpr (FIX && d > 1) sg = (sg & 0x80000000u) | (ds_ones(g) & fixm);  // the row's a == 1 edges (ds_fix_one)
     if constexpr (d == 1) {
         g[0] = ds_out(0.0f, 1.0f, 0u, clamp);  // empty product: p = 1 -> the ceiling, positive
     } else if constexpr (d > DS_SPLIT_D) {
@@ -494,8 +499,8 @@ __host__ __device__ inline uint8_t* qc_sp_zflag(uint32_t* zlist, int64_t B) {
 }
 int qc_sp_fork(const float* llr, int64_t B, int n, int cpu, hipStream_t st, hipStream_t* s2);
 int qc_sp_join(hipStream_t st);
-// up to 3 extra streams per host thread and device, forked from / joined back into the caller's stream by events
-// (graph-capturable); one fork / join pair at a time per thread (qc.hip)
+// up to 3 extra streams per (host thread, device, caller stream), forked from / joined back into the caller's stream
+// by events (graph-capturable); one fork / join pair at a time per caller stream and thread (qc.hip)
 int aux_fork(hipStream_t st, hipStream_t* s2, int n = 1);
 int aux_join(hipStream_t st, int n = 1);
 constexpr unsigned kSpPass2Blocks = 1280;  // second-pass grid cap: 5 units per CU

@@ -366,10 +366,26 @@ __global__ __launch_bounds__(256) void k_vn_spw(const int32_t* __restrict__ var_
         }
 }
 
+// zf[b] = 1 iff codeword b's LLRs hold an exact zero (+-0): the codewords the a == 1 rule applies to (common.h, the
+// rule is per codeword).  One wave per codeword; the same test as the register kernels' k_sp_zero_scan.
+template <int = 0>
+__global__ __launch_bounds__(256) void k_zero_flags(const float* __restrict__ llr, int64_t B, int n,
+                                                    uint8_t* __restrict__ zf) {
+    const int64_t b = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (b >= B) return;  // wave-uniform
+    const int lane = threadIdx.x & 63;
+    const float* p = llr + b * n;
+    bool z = false;
+    for (int i = lane; i < n; i += 64) z |= p[i] == 0.0f;
+    const bool any = __ballot(z) != 0;
+    if (lane == 0) zf[b] = any ? 1 : 0;
+}
+
 template <typename T, int MAXD, bool ES, int V>
 __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_ptr, const T* __restrict__ v2c,
                                                T* __restrict__ c2v, int64_t B, int64_t ldb, T clamp,
-                                               const uint8_t* __restrict__ done, int nodes, int tpl2) {
+                                               const uint8_t* __restrict__ done, int nodes, int tpl2,
+                                               const uint8_t* __restrict__ zf) {
     int c;
     int64_t cw;
     if (!tile_slot<V>(nodes, tpl2, B, c, cw)) return;
@@ -399,13 +415,15 @@ __global__ __launch_bounds__(256) void k_cn_sp(const int32_t* __restrict__ row_p
             }
         });
         DSet pre[V];
-        int n1[V];  // edges with a == 1: every other edge outputs exactly +-0 (common.h ds_fix_ones)
+        int n1[V];  // edges with a == 1: every other edge outputs exactly +-0 (common.h ds_fix_one), in the codewords
+                    // whose LLRs hold an exact zero (zf: the rule is per codeword); none counted elsewhere
 #pragma unroll
         for (int i = 0; i < V; ++i) {
             pre[i] = ds_identity();
             n1[i] = 0;
+            const bool fx = zf[cw + i] != 0;
 #pragma unroll
-            for (int k = 0; k < MAXD; ++k) n1[i] += (k < d && fabsf(t[k].x[i]) == 1.0f) ? 1 : 0;
+            for (int k = 0; k < MAXD; ++k) n1[i] += (fx && k < d && fabsf(t[k].x[i]) == 1.0f) ? 1 : 0;
         }
         static_for<0, MAXD>([&](auto ee) __attribute__((always_inline)) {
             constexpr int e = decltype(ee)::value;
@@ -595,7 +613,7 @@ static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 // Workspace: L[n][ldb], v2c[E][ldb], c2v[E][ldb] (elem bytes each) and, with early stop,
 // hb[n][ldb] (uint8 hard decisions), done[ldb], unsat[ldb], used[ldb] (int32 scratch).
 struct WsLayout {
-    size_t L, v2c, c2v, hb, done, unsat, used, total;
+    size_t L, v2c, c2v, hb, done, unsat, used, zf, total;
 };
 static WsLayout layout(const GenericArgs& g, int64_t B, size_t elem, bool es) {
     const int64_t ldb = (B + 63) / 64 * 64;
@@ -617,6 +635,8 @@ static WsLayout layout(const GenericArgs& g, int64_t B, size_t elem, bool es) {
         w.used = off;
         off += a256((size_t)ldb * 4);
     }
+    w.zf = off;  // fp32 tanh-SP: one byte per codeword, an exact-zero LLR (the a == 1 rule's codewords, k_zero_flags)
+    off += a256((size_t)ldb);
     w.total = off;
     return w;
 }
@@ -671,6 +691,9 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
     const unsigned gcw = (unsigned)((B + kTB - 1) / kTB);
     const T unit = (!MS && std::is_same_v<T, float>) ? T(kLog2eF32) : T(1);  // fp32 tanh-SP messages: log2 units
     k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.n + 63) / 64), tb, 0, st>>>(llr_dev, L, B, g.n, ldb, T(-1));
+    uint8_t* zf = (uint8_t*)(ws + w.zf);
+    if constexpr (!MS && std::is_same_v<T, float>)
+        k_zero_flags<><<<(unsigned)((B + 3) / 4), tb, 0, st>>>((const float*)llr_dev, B, g.n, zf);
     // non-zero initial messages x (bp/bp.py:43-47): iteration 0 reads them like any later iteration
     const T* x0 = wts ? (const T*)wts->c2v0 : nullptr;
     if (x0) k_load_llr<T><<<dim3((unsigned)((B + 63) / 64), (g.E + 63) / 64), tb, 0, st>>>(x0, c2v, B, g.E, ldb, unit);
@@ -742,7 +765,7 @@ static int run(const GenericArgs& g, const T* llr_dev, int64_t B, const ldpc_par
             k_cn_ms<D, ES, VV><<<grid(VV, tpl2, g.m), tb, 0, st>>>(g.row_ptr, (const float*)v2c, (float*)c2v, B, ldb, \
                 p.clamp, p.alpha, p.beta, done, g.m, tpl2);                                                        \
         else                                                                                                       \
-            k_cn_sp<T, D, ES, VV><<<grid(VV, tpl2, g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp, done, g.m, tpl2); \
+            k_cn_sp<T, D, ES, VV><<<grid(VV, tpl2, g.m), tb, 0, st>>>(g.row_ptr, v2c, c2v, B, ldb, clamp, done, g.m, tpl2, zf); \
     } while (0)
 #define CN(D)                                                      \
     do {                                                           \

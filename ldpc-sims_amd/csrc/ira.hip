@@ -78,6 +78,12 @@ __device__ __forceinline__ bool ira_task(int T, int Bc, int& cw, int& task) {
     return cw < Bc;
 }
 
+// IRA_VN_ROT (A/B knob, off): the ascending-order sum by a barrel rotation of the d c2v values (log2 d select stages —
+// which the compiler turns into a compare chain per output, ~150 v_cmp / v_cndmask pairs with s_nop hazard waits
+// per degree-8 task) instead of two masked passes (ira_vn_info)
+#ifndef IRA_VN_ROT
+#define IRA_VN_ROT 0
+#endif
 // c'[i] = c[(i + rho) mod D], rho < D, by log2(D) stages of selects (rotations compose additively mod D)
 template <int D>
 __device__ __forceinline__ void rotate_left(float (&c)[D], int rho) {
@@ -136,38 +142,50 @@ struct IraEs {
     int it;         // the iteration of this launch
 };
 
-// app of information variable (g, pos) of degree D: L + its c2v in ascending check order
+// app of information variable (g, pos) of degree D: L + its c2v in ascending check order.  The table row is sorted by
+// x = a + q s, i.e. by s, so the entries whose position wraps (b = s + pos >= 360: the smaller check indices) are a
+// suffix of it, and the ascending order is: the wrapped entries in table order, then the others in table order —
+// summed as two masked passes (x + (-0) == x bit for bit, so a skipped entry changes nothing), 4 VALU per entry.
+// The state of check (ra, b) is addressed by a 32-bit byte offset from the codeword's first state (a scalar base).
 template <int D>
 __device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int64_t vo, int64_t so, int pos,
                                             const float* __restrict__ L, const IraState* __restrict__ S,
                                             float* __restrict__ app) {
     const int p = min(pos, kIZ - 1);
     const float a = L[vo + p];
+    const char* const Sb = reinterpret_cast<const char*>(S + so);
     float c[D];
+    bool w[D];
     int wrapped = 0;
     static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
         constexpr int t = decltype(TT)::value;
         const int e = row[t];  // wave-uniform: a scalar load
         const int ra = e & 0xff, sh = (e >> 8) & 0x1ff, slot = e >> 17;
         int b = p + sh;
-        const bool w = b >= kIZ;
-        b -= w ? kIZ : 0;
-        wrapped += w;
-        const int64_t i = so + (int64_t)ra * kIZ + b;
+        w[t] = b >= kIZ;
+        b -= w[t] ? kIZ : 0;
+        wrapped += w[t];
+        const uint32_t off = (uint32_t)(ra * kIZ + b) * (uint32_t)sizeof(IraState);
 #if IRA_DIAG_VN4
-        const float x = reinterpret_cast<const float*>(S)[i];
+        const float x = reinterpret_cast<const float*>(S)[so + (int64_t)ra * kIZ + b];
         c[t] = ira_c2v(IraState{x, x, (uint32_t)slot << 27}, slot);
 #else
-        c[t] = ira_c2v(ira_ld(S + i), slot);
+        c[t] = ira_c2v(ira_ld(reinterpret_cast<const IraState*>(Sb + off)), slot);
 #endif
     });
-    // entries are sorted by x = a + q s, i.e. by s: the wrapped ones are the last `wrapped` entries and their
-    // checks come first in ascending order
+    float sum = a;
+#if IRA_VN_ROT
     const int rho = wrapped == 0 ? 0 : D - wrapped;
     rotate_left<D>(c, rho);
-    float sum = a;
 #pragma unroll
     for (int t = 0; t < D; ++t) sum = sum + c[t];
+#else
+    (void)wrapped;
+#pragma unroll
+    for (int t = 0; t < D; ++t) sum = sum + (w[t] ? c[t] : -0.0f);
+#pragma unroll
+    for (int t = 0; t < D; ++t) sum = sum + (w[t] ? -0.0f : c[t]);
+#endif
     if (pos < kIZ) app[vo + pos] = sum;
 }
 

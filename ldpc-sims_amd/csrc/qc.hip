@@ -1150,7 +1150,8 @@ __global__ __launch_bounds__(256, EARLY ? QC_PH_WAVES_PER_SIMD_EARLY : QC_PH_WAV
 // iters_used = it and its z_it is parked in its own L region of LDS (its lanes keep computing for the
 // wave's other codeword, discarded).  Bitwise equal to the generic path's early stop.
 // PASS (the a == 1 rule, common.h cn_ds_row FIX): k_sp_zero_scan lists the waves whose codewords hold an
-// exact-zero LLR (zlist: [0] = count, [1 ..] = wave ids, then one flag byte per wave — qc_sp_zflag); 1 = the plain
+// exact-zero LLR (zlist: [0] = count, [1 ..] = wave ids, then one flag byte per wave, bit j = its codeword j —
+// qc_sp_zflag); 1 = the plain
 // loop for the unlisted waves (a listed one returns at once), 2 = the FIX loop for the listed waves (a small grid
 // whose waves walk the list, on a second stream beside PASS 1: qc_sp_fork / qc_sp_join) — two kernels, so each
 // keeps its own register allocation; 0 = the plain loop for every wave (QC_SP_FIXZ 0).
@@ -1230,6 +1231,9 @@ __device__ __forceinline__ void qc_sp_st_wave(int64_t wave_listed, const float* 
     // QC_SP_MASK_IDLE (fixed count): idle lanes (z >= Z) sit the iteration loop out, EXEC-masked (as QC_PH_MASK_IDLE)
     const bool loop_lane = !(QC_SP_MASK_IDLE && !EARLY) || z < Z;
     constexpr bool FIX = PASS == 2;
+    // the rule applies per codeword (common.h): this lane's codeword's bit of the unit's flag
+    uint32_t fixm = 0x7fffffffu;
+    if constexpr (FIX) fixm = ((qc_sp_zflag(zlist, B)[wave] >> half) & 1u) ? 0x7fffffffu : 0u;
     if (loop_lane)
     for (int it = 0; it < iters; ++it) {
         if constexpr (EARLY) {
@@ -1383,7 +1387,7 @@ __device__ __forceinline__ void qc_sp_st_wave(int64_t wave_listed, const float* 
             });
             if constexpr (!EARLY && QC_SP_PRIO == 1) __builtin_amdgcn_s_setprio(0);
             cn_ds_row<d, (QC_SP_SERIAL && (!EARLY || (QC_SP_SERIAL_ES_Z64 && Z > 32))) ? QC_SP_SERIAL_STRIDE : 0, 0, DS_BLOCK,
-                      FIX>(g, cmax2);
+                      FIX>(g, cmax2, fixm);
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 constexpr int s = C::SHR[r][t];
@@ -1659,72 +1663,129 @@ uint32_t*& qc_sp_zlist() {
     return f;
 }
 
-// one wave per unit of `cpu` consecutive codewords (n LLRs each, row-major): flag = an exact-zero LLR (+-0) in the
-// unit, listed once.  Reads the batch's LLRs once (B n 4 bytes) so that the a == 1 rule's units can run beside the
-// plain pass instead of after it.
+// one wave per unit of `cpu` (<= 8) consecutive codewords (n LLRs each, row-major): flag = bit j set when codeword j
+// of the unit holds an exact-zero LLR (+-0; the a == 1 rule is per codeword, common.h), the unit listed once when any
+// is.  Reads the batch's LLRs once (B n 4 bytes) so that the a == 1 rule's units can run beside the plain pass
+// instead of after it.
 __global__ __launch_bounds__(256) void k_sp_zero_scan(const float* __restrict__ llr, int64_t B, int n, int cpu,
                                                       int64_t units, uint32_t* __restrict__ zlist) {
     const int64_t u = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (u >= units) return;  // wave-uniform
     const int lane = threadIdx.x & 63;
     const int64_t c0 = u * cpu, c1 = (c0 + cpu < B) ? c0 + cpu : B;
-    const float* p = llr + c0 * n;
-    const int64_t cnt = (c1 - c0) * n;
-    bool z = false;
-    int64_t i0 = 0;
-    if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
-        const float4* p4 = reinterpret_cast<const float4*>(p);
-        const int64_t n4 = cnt >> 2;
-        for (int64_t i = lane; i < n4; i += 64) {
-            const float4 v = p4[i];
-            z |= (v.x == 0.0f) | (v.y == 0.0f) | (v.z == 0.0f) | (v.w == 0.0f);
+    uint32_t mask = 0;
+    for (int64_t c = c0; c < c1; ++c) {
+        const float* p = llr + c * n;
+        bool z = false;
+        int64_t i0 = 0;
+        if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+            const float4* p4 = reinterpret_cast<const float4*>(p);
+            const int64_t n4 = n >> 2;
+            for (int64_t i = lane; i < n4; i += 64) {
+                const float4 v = p4[i];
+                z |= (v.x == 0.0f) | (v.y == 0.0f) | (v.z == 0.0f) | (v.w == 0.0f);
+            }
+            i0 = n4 << 2;
         }
-        i0 = n4 << 2;
+        for (int64_t i = i0 + lane; i < n; i += 64) z |= p[i] == 0.0f;
+        mask |= (__ballot(z) != 0 ? 1u : 0u) << (c - c0);
     }
-    for (int64_t i = i0 + lane; i < cnt; i += 64) z |= p[i] == 0.0f;
-    const bool zu = __ballot(z) != 0;
     if (lane == 0) {
-        qc_sp_zflag(zlist, B)[u] = zu ? 1 : 0;
-        if (zu) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)u;
+        qc_sp_zflag(zlist, B)[u] = (uint8_t)mask;
+        if (mask) zlist[1 + atomicAdd(zlist, 1u)] = (uint32_t)u;
     }
 }
 
 namespace {
+// Auxiliary streams for the forked decodes (the a == 1 rule's pass, the IRA path's Infinity-Cache chunks): kAux
+// streams and their fork / join events per (host thread, device, CALLER stream) — keyed by the caller's stream so
+// that decodes on different caller streams never share an auxiliary stream (no false dependence of one caller's join
+// on another's fork, and a graph capture open on stream A never absorbs a decode issued on stream B), and per host
+// thread so that no two threads interleave one set's fork / join.  At most kAuxSets sets per thread (the least
+// recently used is destroyed — hipStreamDestroy lets its pending work finish); a thread's sets are destroyed when
+// it exits.
 constexpr int kAux = 3;
-struct Aux {  // per host thread and device: kAux extra streams and their fork / join events
+constexpr int kAuxSets = 16;
+struct Aux {
+    int dev = -1;
+    hipStream_t caller = nullptr;
+    uint64_t used = 0;  // LRU stamp
     hipStream_t s[kAux] = {};
     hipEvent_t fork = nullptr, join[kAux] = {};
-    bool ready = false;
-};
-Aux* aux_get() {
-    static thread_local Aux aux[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    Aux& a = aux[dev];
-    if (!a.ready) {
-        if (!a.fork && hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) != hipSuccess) {
-            a.fork = nullptr;
-            return nullptr;
+    void release() {
+        for (int i = 0; i < kAux; ++i) {
+            if (s[i]) (void)hipStreamDestroy(s[i]);
+            if (join[i]) (void)hipEventDestroy(join[i]);
+            s[i] = nullptr;
+            join[i] = nullptr;
+        }
+        if (fork) (void)hipEventDestroy(fork);
+        fork = nullptr;
+        dev = -1;
+        caller = nullptr;
+    }
+    bool create() {
+        if (hipEventCreateWithFlags(&fork, hipEventDisableTiming) != hipSuccess) {
+            fork = nullptr;
+            return false;
         }
         for (int i = 0; i < kAux; ++i) {
-            if (!a.s[i] && hipStreamCreateWithFlags(&a.s[i], hipStreamNonBlocking) != hipSuccess) {
-                a.s[i] = nullptr;
-                return nullptr;
+            if (hipStreamCreateWithFlags(&s[i], hipStreamNonBlocking) != hipSuccess) {
+                s[i] = nullptr;
+                return false;
             }
-            if (!a.join[i] && hipEventCreateWithFlags(&a.join[i], hipEventDisableTiming) != hipSuccess) {
-                a.join[i] = nullptr;
-                return nullptr;
+            if (hipEventCreateWithFlags(&join[i], hipEventDisableTiming) != hipSuccess) {
+                join[i] = nullptr;
+                return false;
             }
         }
-        a.ready = true;
+        return true;
     }
-    return &a;
+};
+struct AuxPool {
+    Aux set[kAuxSets];
+    uint64_t clock = 0;
+    ~AuxPool() {
+        for (Aux& a : set)
+            if (a.dev >= 0) a.release();
+    }
+};
+Aux* aux_get(hipStream_t caller) {
+    static thread_local AuxPool pool;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    Aux* lru = &pool.set[0];
+    for (Aux& a : pool.set) {
+        if (a.dev == dev && a.caller == caller) {
+            a.used = ++pool.clock;
+            return &a;
+        }
+        if (a.used < lru->used) lru = &a;
+    }
+    if (lru->dev >= 0) lru->release();
+    if (!lru->create()) {
+        lru->release();
+        return nullptr;
+    }
+    lru->dev = dev;
+    lru->caller = caller;
+    lru->used = ++pool.clock;
+    return lru;
+}
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
 }
 }  // namespace
 
 int aux_fork(hipStream_t st, hipStream_t* s2, int n) {
-    Aux* a = aux_get();
+    Aux* a = aux_get(st);
     if (!a || n < 1 || n > kAux) return set_error(LDPC_EHIP, "auxiliary streams unavailable");
+    // an auxiliary stream still inside a capture the caller is not part of (a capture that ended abnormally) would
+    // record this decode into that graph
+    if (!capturing(st))
+        for (int i = 0; i < n; ++i)
+            if (capturing(a->s[i])) return set_error(LDPC_EHIP, "auxiliary stream is inside another stream's graph capture");
     if (hipEventRecord(a->fork, st) != hipSuccess) return set_error(LDPC_EHIP, "auxiliary stream: fork failed");
     for (int i = 0; i < n; ++i) {
         if (hipStreamWaitEvent(a->s[i], a->fork, 0) != hipSuccess)
@@ -1735,7 +1796,7 @@ int aux_fork(hipStream_t st, hipStream_t* s2, int n) {
 }
 
 int aux_join(hipStream_t st, int n) {
-    Aux* a = aux_get();
+    Aux* a = aux_get(st);
     if (!a || n < 1 || n > kAux) return set_error(LDPC_EHIP, "auxiliary streams unavailable");
     for (int i = 0; i < n; ++i)
         if (hipEventRecord(a->join[i], a->s[i]) != hipSuccess || hipStreamWaitEvent(st, a->join[i], 0) != hipSuccess)

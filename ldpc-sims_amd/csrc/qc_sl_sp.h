@@ -190,6 +190,9 @@ __device__ __forceinline__ void qc_sp_sl_unit(uint32_t unit_listed, const float*
     int used0 = iters, used1 = iters;
 
     constexpr bool FIX = PASS == 2;
+    // the rule applies per codeword (common.h): this lane's codeword's bit of the unit's flag
+    uint32_t fixm = 0x7fffffffu;
+    if constexpr (FIX) fixm = ((qc_sp_zflag(zlist, B)[unit] >> h) & 1u) ? 0x7fffffffu : 0u;
     for (int it = 0; it < iters; ++it) {
         if constexpr (EARLY) {
             if (it > 0) {
@@ -286,7 +289,7 @@ __device__ __forceinline__ void qc_sp_sl_unit(uint32_t unit_listed, const float*
                 if constexpr (s == 0) g[t] = msg[e0 + t];
                 else g[t] = Xv[nz_index<C>(r, t) * ROW + xb + s];
             });
-            cn_ds_row<d, QC_SL_SP_SERIAL_ROW, 0, DS_BLOCK, FIX>(g, cmax2);  // O(d) exclusive sets (common.h)
+            cn_ds_row<d, QC_SL_SP_SERIAL_ROW, 0, DS_BLOCK, FIX>(g, cmax2, fixm);  // O(d) exclusive sets (common.h)
             if constexpr (CMP) sl_barrier();  // every wave has read this row's v2c before the buffer takes its c2v
             if (live) {
                 static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
@@ -551,6 +554,9 @@ __device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float*
     // keeps live lanes, so each still meets both barriers of every iteration)
     const bool loop_lane = !QC_RS_MASK_IDLE || live;
     constexpr bool FIX = PASS == 2;
+    // the rule applies per codeword (common.h): this lane's codeword's bit of the unit's flag
+    uint32_t fixm = 0x7fffffffu;
+    if constexpr (FIX) fixm = ((qc_sp_zflag(zlist, B)[unit] >> h) & 1u) ? 0x7fffffffu : 0u;
     if (loop_lane)
     for (int it = 0; it < iters; ++it) {
         // VN phase (variable frame): every column's c2v -> v2c as signed a, written back in place
@@ -624,7 +630,7 @@ __device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float*
             });
             if constexpr (QC_RS_PRIO == 3) __builtin_amdgcn_s_setprio(0);
             if constexpr (QC_RS_CPF > 0 && r + 1 < MB) cpf(std::integral_constant<int, r + 1>{});
-            cn_ds_row<d, QC_RS_SERIAL_ROW, QC_RS_ROW_LAG, QC_RS_DS_BLOCK, FIX>(g, cmax2);  // O(d) exclusive sets (common.h)
+            cn_ds_row<d, QC_RS_SERIAL_ROW, QC_RS_ROW_LAG, QC_RS_DS_BLOCK, FIX>(g, cmax2, fixm);  // O(d) exclusive sets (common.h)
             static_for<0, d>([&](auto tt) __attribute__((always_inline)) {
                 constexpr int t = decltype(tt)::value;
                 if constexpr (C::SHR[r][t] == 0) m0[rs_zero_index<C>(r, t)] = g[t];

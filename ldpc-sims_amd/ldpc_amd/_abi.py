@@ -22,8 +22,9 @@ EXPORTS = (
     "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
     "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_adc_quantize", "ldpc_weights_layout",
     "ldpc_decode_weighted", "ldpc_decode_x0", "ldpc_decode_bits_host", "ldpc_last_error", "ldpc_device_count",
-    "ldpc_version", "ldpc_kernel_path",
+    "ldpc_version", "ldpc_kernel_path", "ldpc_abi_version",
 )
+ABI_VERSION = 2  # LDPC_ABI_VERSION of include/ldpc_abi.h this binding is written for
 
 
 class LdpcError(RuntimeError):
@@ -66,6 +67,13 @@ def load(path: str | None = None):
         raise ImportError(f"{p} not found: the HIP decoder is not built (run `python __graft_entry__.py`); "
                           "there is no CPU fallback")
     L = ctypes.CDLL(p)
+    try:
+        got = ctypes.CFUNCTYPE(ctypes.c_int)(("ldpc_abi_version", L))()
+    except AttributeError:
+        got = 1  # revision 1 libraries predate the symbol
+    if got != ABI_VERSION:
+        raise ImportError(f"{p}: ABI revision {got}, this binding needs {ABI_VERSION} (include/ldpc_abi.h "
+                          "LDPC_ABI_VERSION); rebuild the library")
     vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
     gpp = ctypes.POINTER(ctypes.c_void_p)
     L.ldpc_graph_create.argtypes = [i32, i32, i32, vp, vp, i32, gpp]
@@ -90,7 +98,7 @@ def load(path: str | None = None):
     for f in ("ldpc_graph_create", "ldpc_graph_create_qc", "ldpc_graph_destroy", "ldpc_graph_info",
               "ldpc_workspace_size", "ldpc_decode_ex", "ldpc_decode", "ldpc_count_errors", "ldpc_awgn_llr",
               "ldpc_random_bits", "ldpc_ofdm_tx", "ldpc_ofdm_demod", "ldpc_adc_quantize", "ldpc_weights_layout", "ldpc_decode_weighted",
-              "ldpc_decode_x0", "ldpc_decode_bits_host", "ldpc_device_count"):
+              "ldpc_decode_x0", "ldpc_decode_bits_host", "ldpc_device_count", "ldpc_abi_version"):
         getattr(L, f).restype = ctypes.c_int
     L.ldpc_last_error.restype = ctypes.c_char_p
     L.ldpc_version.restype = ctypes.c_char_p

@@ -85,7 +85,10 @@ static int syndrome_ok(const graph_t* g, const uint8_t* bits);
  * whose output is then log 1 = 0: an edge whose exclusive set holds an a == 1 edge outputs exactly 0 (its sign
  * bit as any other output's).  (Pushes and a join with such a suffix keep D == S exactly, but the fma join with
  * such a prefix only to an ulp, which several zeros per check — erasures, quantized LLRs — add up to a flipped
- * hard decision: tests/golden/bp_zeros.npz.)
+ * hard decision: tests/golden/bp_zeros.npz.)  The rule is PER CODEWORD (fixz, round 6): it applies to a codeword
+ * whose LLRs hold an exact zero (+-0) — the source of s = +-0 — for all its iterations, and not at all to the
+ * others, where an a == 1 edge (an exact cancellation, or |s| so small that exp2 rounds to 1) keeps the plain
+ * (D, S) outputs, within 2^-23 of 0; every GPU kernel applies the same rule (csrc/common.h).
  * Messages in LOG2 UNITS, as the GPU kernels keep them (ldpc-sims_amd/csrc/common.h): s2 = fma(L, log2 e, sum2),
  * a = exp2(-|s2|), the check output log2(S/D) clamped to [0, cmax2] with cmax2 = min(fp32(clamp * log2 e), 24 =
  * fp32(log2 RMAX)), z = fma(sum2, fp32(ln 2 / 2), 0.5 * L).  The trace reports messages in natural units (x ln 2). */
@@ -94,7 +97,7 @@ static int syndrome_ok(const graph_t* g, const uint8_t* bits);
 #define LN2_F32 0.693147182f       /* fp32(ln 2) */
 #define CEIL_LOG2_F32 24.0f        /* fp32(log2 16777215) */
 static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float cmax2, float* out,
-                          float* sufD, float* sufS) {
+                          float* sufD, float* sufS, int fixz) {
     if (d == 0) return;  /* an empty check (all-zero row of H) has no edges */
     if (d == 1) {  /* empty product = 1 -> the p clamp: S/D = 1/0 -> the ceiling */
         out[0] = cmax2;
@@ -104,7 +107,7 @@ static void cn_stable_f32(int d, const float* sa /* signed a per edge */, float 
     int n1 = 0;  /* edges with a == 1 */
     for (int t = 0; t < d; ++t) {
         sg ^= f2u(sa[t]);
-        n1 += fabsf(sa[t]) == 1.0f;
+        n1 += fixz && fabsf(sa[t]) == 1.0f;
     }
     sufD[d - 1] = fabsf(sa[d - 1]);
     sufS[d - 1] = 1.0f;
@@ -139,6 +142,8 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
     const int E = g->E;
     int used = iters;
     const float c2 = clamp * LOG2E_F32, cmax2 = c2 < CEIL_LOG2_F32 ? c2 : CEIL_LOG2_F32;
+    int fixz = 0;  /* an exact-zero LLR: the a == 1 rule's codewords (cn_stable_f32) */
+    for (int v = 0; v < g->n; ++v) fixz |= llr[v] == 0.0f;
     for (int e = 0; e < E; ++e) x[e] = 0.0f;
     for (int it = 0; it < iters; ++it) {
         if (early_stop && it > 0) {
@@ -204,7 +209,7 @@ static int sp_f32_one(const graph_t* g, const float* llr, int iters, float clamp
         /* CV */
         for (int c = 0; c < g->m && stable; ++c) {
             const int a = g->row_ptr[c], b = g->row_ptr[c + 1];
-            cn_stable_f32(b - a, v2c + a, cmax2, x + a, sufD, sufS);
+            cn_stable_f32(b - a, v2c + a, cmax2, x + a, sufD, sufS, fixz);
         }
         for (int c = 0; c < g->m && !stable; ++c) {
             const int a = g->row_ptr[c], b = g->row_ptr[c + 1];

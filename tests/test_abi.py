@@ -52,5 +52,25 @@ def test_argument_validation_without_gpu():
     assert lib.ldpc_device_count() >= 0
 
 
+def test_abi_revision_matches_header_and_binding():
+    """ldpc_decode's signature changed in round 5 (iters_used before the stream): the library reports the
+    header's LDPC_ABI_VERSION and the binding refuses any other revision."""
+    src = open(os.path.join(ROOT, "include", "ldpc_abi.h")).read()
+    hdr = int(re.search(r"#define LDPC_ABI_VERSION (\d+)", src).group(1))
+    lib = _abi.load()
+    assert lib.ldpc_abi_version() == hdr == _abi.ABI_VERSION == 2
+
+
+def test_loader_refuses_other_abi_revision(tmp_path):
+    import subprocess
+    so = tmp_path / "libold.so"
+    c = tmp_path / "old.c"
+    c.write_text("int ldpc_abi_version(void) { return 1; }\n")
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(c)])
+    import pytest
+    with pytest.raises(ImportError, match="ABI revision 1"):
+        _abi.load(str(so))
+
+
 def test_params_struct_layout():
     assert ctypes.sizeof(_abi.Params) == 36

@@ -52,3 +52,13 @@ def test_bench_line_contract():
         assert abs(lg["value"] - b / (lg["ms_per_step"] / 1e3)) <= 1e-6 * lg["value"]
         for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_ms"):
             assert k in lg["roofline"], (name, k)
+        assert "clock" in lg
+    # config [4]'s bytes are served beyond L2 mostly by the Infinity Cache: labelled so, HBM fraction beside it
+    r4 = legs["config4"]["roofline"]
+    assert r4["bound"].startswith("memory-side") and r4["peak"] == 8600.0 and 0 < r4["hbm_frac"]
+    # the engine clock over the timed loop (amdsmi gpu_metrics), or the reason it could not be read
+    clk = d["clock"]
+    assert "clock_mhz" in clk or "error" in clk, clk
+    if "clock_mhz" in clk:
+        assert 500 < clk["clock_mhz"] <= 2500 and clk["samples"] >= 1
+    assert d["ranks"]["per_rank"][0]["clock"] == clk

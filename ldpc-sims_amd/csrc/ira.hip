@@ -273,11 +273,15 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
         const float ap1 = prc[pi];
         const bool fuse = FUSE && ra > tb * tpw;  // parity (ra - 1, p): both its checks' new states are here
         const float lp = fuse ? L[ao + t.k + (int64_t)(ra - 1) * kIZ + p] : 0.0f;
+        // the row's table entries as one scalar load before any use (inside the per-slot branches each entry was
+        // its own load and wait, and each slot's posterior load waited on it)
+        int ent[MAXR];
+        static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) { ent[decltype(SS)::value] = row[decltype(SS)::value]; });
         float v[MAXR];
         static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
             constexpr int s = decltype(SS)::value;
             if (s < R) {
-                const int e = row[s];
+                const int e = ent[s];
                 const int g = e & 0xff, sh = e >> 8;
                 int m = p - sh;
                 m += m < 0 ? kIZ : 0;
@@ -298,16 +302,16 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
         float min1 = __builtin_inff(), min2 = __builtin_inff();
         int idx = -1;
         uint32_t sgn = 0;
+        // branch-free two-minimum (as written with if / else-if the compiler made every slot a divergent branch with
+        // exec-mask saves and register shuffles): m < min1 -> (m, min1, s); else min2 = min(min2, m) — the same
+        // values, magnitudes being >= +0 and never NaN
         auto take = [&](float x, int s) __attribute__((always_inline)) {
             const float m = fabsf(x);
             sgn ^= f2u(x);
-            if (m < min1) {
-                min2 = min1;
-                min1 = m;
-                idx = s;
-            } else if (m < min2) {
-                min2 = m;
-            }
+            const bool lt = m < min1;
+            min2 = lt ? min1 : fminf(min2, m);
+            min1 = lt ? m : min1;
+            idx = lt ? s : idx;
         };
         static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
             constexpr int s = decltype(SS)::value;
@@ -519,9 +523,12 @@ bool ira_supports(const IRASpec* s, const ldpc_params& p) {
 // Infinity Cache for all their iterations; LDPC_IRA_BUDGET_MB overrides (0 = the whole batch in one pass).  Config
 // [4], B = 4,096, one stream (profiles/r05/ab/ab_c4_ira_tpw.txt): 100 MB 28.2k cw/s, 200 MB 32.8k, 240 MB 33.6k,
 // 256 MB 34.0k, 400 MB 25.2k; two streams: 200 MB 41.55k, 256 MB 41.3k, 320 MB 35.5k (ab_c4_ira_streams.txt).
+// Round 6, after the variable sums without the rotation network and the branch-free check kernel (two streams,
+// profiles/r06/ab/ab_c4_ira_vn_cn.txt): 200 MB 59.1k, 230 MB 59.5k, 250 MB 59.7k, 270 MB 46.3k (out of the Infinity
+// Cache): 240 shipped, clear of the cliff.
 static int64_t ira_chunk(const IRASpec* s, int64_t B, int ns = 1) {
     const char* env = getenv("LDPC_IRA_BUDGET_MB");
-    const int64_t budget = ((env ? (int64_t)atol(env) : 200) << 20) / ns;
+    const int64_t budget = ((env ? (int64_t)atol(env) : 240) << 20) / ns;
     if (budget <= 0) return B;
     const int64_t per = 8 * (int64_t)s->n + 12 * (int64_t)s->M + (IRA_CNPAR ? 4 * (int64_t)s->M : 0);
     int64_t bc = budget / per / 8 * 8;

@@ -356,11 +356,20 @@ class Workload:
                 "ebn0": a.ebn0, "seed": a.seed,
                 "batch_per_gpu": self.B, "global_batch": self.B * world,
                 "parallelism": f"dp{world} (codeword shards, RCCL all-reduce of error counts only)",
-                "kernel_path": self.kpath}
+                "kernel_path": self.kpath,
+                # the library's tuning knobs set in the environment (LDPC_*: chunk budget, streams, a variant
+                # library, ...): empty for the shipped configuration; a counter record must match it
+                "env": library_env()}
 
     def free(self):
         self.llrs = []
         self.cw = self.ws = self.bits = None
+
+
+def library_env():
+    """LDPC_* environment overrides of the library's defaults in this process (bench's own LDPC_BENCH_* launch knobs
+    excluded: they place ranks, not kernels)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("LDPC_") and not k.startswith("LDPC_BENCH_")}
 
 
 def rank_evidence(world, rank, local, elapsed, clock=None):
@@ -419,7 +428,7 @@ def roofline(n, E, B, launch_ms, args, kpath, m=None, iters=None):
     note = None
     if os.path.exists(args.counters_json):
         want = {"code": args.code, "algo": args.algo, "iters": args.iters, "early_stop": args.early_stop,
-                "batch_per_gpu": B, "kernel_path": kpath, "mod": args.mod}
+                "batch_per_gpu": B, "kernel_path": kpath, "mod": args.mod, "env": library_env()}
         if args.early_stop:  # the work done depends on the data (iterations to convergence): same grid and seed
             want.update(ebn0=args.ebn0, seed=args.seed)
         for r in json.load(open(args.counters_json)):

@@ -147,8 +147,15 @@ __device__ __forceinline__ float sp_vn_arg(float L, float sum2) { return __built
 #ifndef DS_CR
 #define DS_CR 0
 #endif
+// DS_DIAG_NOTRANS (DIAGNOSTIC BUILDS ONLY, wrong results): the three transcendentals (v_exp_f32 here, v_rcp_f32 and
+// v_log_f32 in ds_out) replaced by one fma each, to price what their issue cost and latency take from a kernel
+#ifndef DS_DIAG_NOTRANS
+#define DS_DIAG_NOTRANS 0
+#endif
 __device__ __forceinline__ float vn_signed_a(float x2) {
-#if DS_CR & 1
+#if DS_DIAG_NOTRANS
+    return __builtin_copysignf(__builtin_fmaf(-fabsf(x2), 0x1p-6f, 1.0f), x2);
+#elif DS_CR & 1
     return __builtin_copysignf((float)exp2(-(double)fabsf(x2)), x2);
 #else
     return __builtin_copysignf(__builtin_amdgcn_exp2f(-fabsf(x2)), x2);
@@ -211,12 +218,16 @@ __device__ __forceinline__ DSet ds_push(DSet x, float a) {  // a = |signed a| of
 // log2(S/D) of a set clamped to [0, cmax2] (S >= D; a rounding below 1 gives 0; D == 0: +inf -> cmax2), with
 // the given sign bit (bit 31 of sgn)
 __device__ __forceinline__ float ds_out(float D, float S, uint32_t sgn, float cmax2) {
-#if DS_CR & 2
+#if DS_DIAG_NOTRANS
+    const float r = __builtin_fmaf(S, 0.5f, D);
+#elif DS_CR & 2
     const float r = (float)((double)S / (double)D);  // S, D exact in fp64: one rounding = the oracle's S / D
 #else
     const float r = S * __builtin_amdgcn_rcpf(D);
 #endif
-#if DS_CR & 4
+#if DS_DIAG_NOTRANS
+    const float y = __builtin_amdgcn_fmed3f(__builtin_fmaf(r, 0.25f, -1.0f), 0.0f, cmax2);
+#elif DS_CR & 4
     const float y = __builtin_amdgcn_fmed3f((float)log2((double)r), 0.0f, cmax2);
 #else
     const float y = __builtin_amdgcn_fmed3f(__builtin_amdgcn_logf(r), 0.0f, cmax2);

@@ -439,6 +439,10 @@ constexpr int rs_q() {  // the smallest Q with Q * Q >= Z (9 for 81)
     return q;
 }
 
+// QC_RS_DIAG_NOBAR (DIAGNOSTIC BUILDS ONLY, wrong results): the two barriers per iteration removed, to price them
+#ifndef QC_RS_DIAG_NOBAR
+#define QC_RS_DIAG_NOBAR 0
+#endif
 template <class C, int PASS>  // PASS, unit_listed: as qc_sp_sl_unit's
 __device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float* __restrict__ llr, int64_t B, int iters,
                                               float clamp, int flags, uint8_t* __restrict__ bits,
@@ -603,7 +607,7 @@ __device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float*
                 });
             }
         });
-        __syncthreads();
+        if constexpr (!QC_RS_DIAG_NOBAR) __syncthreads();  // (QC_RS_DIAG_NOBAR: diagnostic builds only)
         // CN phase (check frame): every row's v2c -> c2v, written back in place
         if constexpr (QC_RS_PRIO == 1 || QC_RS_PRIO == 3 || QC_RS_PRIO == 4) __builtin_amdgcn_s_setprio(0);
         if constexpr (QC_RS_PRIO == 2) __builtin_amdgcn_s_setprio(1);
@@ -641,7 +645,7 @@ __device__ __forceinline__ void qc_sp_rs_unit(uint32_t unit_listed, const float*
                 });
             }
         });
-        __syncthreads();
+        if constexpr (!QC_RS_DIAG_NOBAR) __syncthreads();  // (QC_RS_DIAG_NOBAR: diagnostic builds only)
     }
     // the output's lane coordinates recomputed after the loop — the lane id by v_mbcnt (the work-item id VGPR of
     // the launch is long gone), the slot wave k is scalar — instead of kept across it: the values set before the

@@ -16,7 +16,8 @@ NAME=${NAME:-headline}
 ARGS="${ARGS:-} --no-dropin --no-legs"  # side measurements and the other configs' legs are not profiled
 GRID=$(python3 -c "import sys; a=sys.argv[1:]; print(a[a.index('--ebn0')+1] if '--ebn0' in a else '0:0.5:5')" $ARGS)
 P=$(python3 -c "import numpy as np,sys; lo,s,hi=map(float,sys.argv[1].split(':')); print(len(np.arange(lo,hi+1e-9,s)))" $GRID)
-PARGS="--steps $P --warmup $P --no-cpu-baseline"
+S=${STEPS:-$P}  # timed decodes (default: one per Eb/N0 point); the summary keeps the timed loop's S launches
+PARGS="--steps $S --warmup $S --no-cpu-baseline"
 if [ -n "$DKERNELS" ]; then SEL="--decode-kernels $DKERNELS --chunks ${CHUNKS:-1}"; else SEL="--kernel ${KERNEL:-k_qc_ms}"; fi
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
 P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE"
@@ -31,4 +32,4 @@ for grp in "$P1" "$P2" FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d $D/pmc$i -o run -- python3 bench.py $ARGS $PARGS > $D/pmc$i.json 2> $D/pmc$i.err || { echo "pmc pass $i ($NAME) failed"; tail -5 $D/pmc$i.err; exit 1; }
   echo "  pmc pass $i done"
 done
-python3 scripts/counters_summary.py $D --name $NAME $SEL --last $P > $OUT/counters_$NAME.json && echo "counters_$NAME.json written"
+python3 scripts/counters_summary.py $D --name $NAME $SEL --last $S > $OUT/counters_$NAME.json && echo "counters_$NAME.json written"

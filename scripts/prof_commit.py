@@ -25,6 +25,10 @@ def main():
     a = ap.parse_args()
     os.makedirs(a.dst, exist_ok=True)
     shutil.copy(os.path.join(a.src, "bench.json"), os.path.join(a.dst, "bench.json"))
+    for f in glob.glob(os.path.join(a.src, "**", "*kernel_stats.csv"), recursive=True):  # the rocprofv3 --stats summary
+        out = os.path.join(a.dst, os.path.relpath(f, a.src))
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        shutil.copy(f, out)
     pats = [p for p in a.decode.split(",") if p]
     files = glob.glob(os.path.join(a.src, "**", "*kernel_trace.csv"), recursive=True)
     files += glob.glob(os.path.join(a.src, "**", "*counter_collection.csv"), recursive=True)

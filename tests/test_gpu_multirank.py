@@ -152,7 +152,7 @@ def test_bench_multigpu_runs_the_config4_leg():
     assert l2["ber"]["codewords_per_point"] == l1["ber"]["codewords_per_point"] == 512
     assert l2["ber"]["coded_ber_info"] == l1["ber"]["coded_ber_info"]
     assert l2["ber"]["coded_bler"] == l1["ber"]["coded_bler"]
-    assert l2["roofline"]["bound"] == "hbm" and l2["roofline"]["frac"] > 0
+    assert l2["roofline"]["bound"].startswith("memory-side") and l2["roofline"]["frac"] > 0  # IRA: Infinity-Cache bytes
 
 
 def test_bench_rccl_process_group_on_one_gpu():

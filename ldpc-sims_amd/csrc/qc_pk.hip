@@ -205,10 +205,20 @@ __device__ __forceinline__ uint32_t xor_all_u(const uint32_t (&v)[D]) {
     return t;
 }
 
+// QC_PK_PAIRS (A/B knob, early stop; default 1): each wave decodes this many codeword pairs one after the other,
+// the body straight-line per pair (no runtime loop around it: round 5's persistent loop had raised the register
+// demand past the 3-waves/SIMD budget), wave w taking pairs w, w + W, ... (W = the grid's waves)
+#ifndef QC_PK_PAIRS
+#define QC_PK_PAIRS 1
+#endif
 template <class C, bool EARLY, bool BETA>
-__global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_PK_WAVES_PER_SIMD) void k_qc_qms_pk(
-    const float* __restrict__ llr, int64_t B, int iters, float qmax, float app_max, float beta, float qinv, int flags,
-    uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
+__device__ __forceinline__ void qms_pk_pair(int64_t wave, const float* __restrict__ llr, int64_t B, int iters, float qmax,
+                                            float app_max, float beta, float qinv, int flags, uint8_t* __restrict__ bits,
+                                            float* __restrict__ soft, int32_t* __restrict__ iters_used, int64_t pair_off) {
+    // the work-item id through an empty asm: every lane-derived value is recomputed per pair (QC_PK_PAIRS > 1)
+    // rather than kept live from one pair's body into the next
+    unsigned tx = threadIdx.x;
+    asm volatile("" : "+v"(tx));
     constexpr int Z = C::Z, NB = C::NB, MB = C::MB, N = NB * Z;
     constexpr int NE = edge_off<C>(MB);
     static_assert(Z <= 64, "packed kernel: one lane group per codeword pair");
@@ -218,11 +228,10 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     constexpr bool LDSROT = EARLY ? QC_PK_LDSROT_EARLY : QC_PK_LDSROT;
     constexpr bool DROT = EARLY ? QC_PK_DROT_EARLY : QC_PK_DROT;
     constexpr bool ILV = QC_PK_ILV && CPW == 1 && Z % 2 == 0 && !LDSROT && !DROT;
-    const int lane = threadIdx.x & 63;
+    const int lane = tx & 63;
     const int half = (CPW == 2) ? (lane >> 5) : 0;
     // lifting index of this lane (>= Z: idle); ILV: even z in the lower half, odd in the upper
     const int z = ILV ? ((lane & 31) < Z / 2 ? 2 * (lane & 31) + (lane >> 5) : Z + (lane & 31)) : ((CPW == 2) ? (lane & 31) : lane);
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t cw0 = (wave * CPW + half) * 2;  // low fp16: cw0, high: cw0 + 1
     const int zb = lane_zb<Z, CPW>(z);
     const int base4 = (half * 32 + zb) * 4;
@@ -233,12 +242,12 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     using f4 = __attribute__((ext_vector_type(4))) float;
     constexpr int LSTR = lstr<C>();
     __shared__ __attribute__((aligned(16))) uint32_t Ls[pk_tpb<EARLY>() * LSTR];  // lane-major packed L rows (lpos)
-    const int lrow = threadIdx.x * LSTR;
+    const int lrow = tx * LSTR;
     const int lrow4 = lrow * 4;  // bytes (lds_reload)
 
     // lane rotations through a per-wave LDS row (as k_qc_ms_ph, qc.hip QC_PH_LDSROT) or ds_bpermute
     __shared__ uint32_t Rw[LDSROT ? pk_tpb<EARLY>() : 1];
-    const int wrow = LDSROT ? (int)(threadIdx.x & ~63u) * 4 : 0;
+    const int wrow = LDSROT ? (int)(tx & ~63u) * 4 : 0;
     const int rb4 = base4 + wrow, rb4m = base4m + wrow;
     if constexpr (LDSROT) {  // M0 = this wave's row, once (nothing else here uses M0); s_nop 0: M0 -> add-TID hazard
         const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&Rw[0]) + (unsigned)wrow);
@@ -271,7 +280,7 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     });
     constexpr int DW = CPW * 2 * Z + 64 + 2 * Z;  // words per wave: doubled rows, then the idle lanes' stretch
     __shared__ uint32_t Rd[DROT ? (pk_tpb<EARLY>() / 64) * DW : 1];
-    const int da = DROT ? 4 * ((int)(threadIdx.x >> 6) * DW + ((z < Z) ? half * 2 * Z + z : CPW * 2 * Z + lane)) : 0;
+    const int da = DROT ? 4 * ((int)(tx >> 6) * DW + ((z < Z) ? half * 2 * Z + z : CPW * 2 * Z + lane)) : 0;
     auto rot = [&](auto rr, uint32_t x) __attribute__((always_inline)) {  // value of lane (z + rho) mod Z
         constexpr int rho = decltype(rr)::value;
         if constexpr (rho == 0) {
@@ -488,12 +497,12 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     // last iteration (or early exit): outputs straight from the VN phase
     const bool early_exit = EARLY && done == ALL;
     if (!early_exit && iters > 0) cn_phase();
-    int tid = threadIdx.x;
+    int tid = tx;
     asm volatile("" : "+v"(tid));
     const int zo = ILV ? ((tid & 31) < Z / 2 ? 2 * (tid & 31) + ((tid >> 5) & 1) : Z + (tid & 31))
                        : ((CPW == 2) ? (tid & 31) : (tid & 63));
     const int go = (CPW == 2) ? ((tid >> 5) & 1) : 0;
-    const int64_t c0 = ((((int64_t)blockIdx.x * blockDim.x + tid) >> 6) * CPW + go) * 2;
+    const int64_t c0 = (((((int64_t)blockIdx.x * blockDim.x + tid) >> 6) + pair_off) * CPW + go) * 2;
     const bool park0 = EARLY && ((done >> (2 * go)) & 1u), park1 = EARLY && ((done >> (2 * go + 1)) & 1u);
     const bool ok0 = zo < Z && c0 < B, ok1 = zo < Z && c0 + 1 < B;
     static_for<0, NB>([&](auto pp) __attribute__((always_inline)) {
@@ -524,13 +533,27 @@ __global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_
     }
 }
 
+template <class C, bool EARLY, bool BETA>
+__global__ __launch_bounds__(QC_PK_TPB, EARLY ? QC_PK_WAVES_PER_SIMD_EARLY : QC_PK_WAVES_PER_SIMD) void k_qc_qms_pk(
+    const float* __restrict__ llr, int64_t B, int iters, float qmax, float app_max, float beta, float qinv, int flags,
+    uint8_t* __restrict__ bits, float* __restrict__ soft, int32_t* __restrict__ iters_used) {
+    constexpr int P = EARLY ? QC_PK_PAIRS : 1;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t W = (int64_t)gridDim.x * (blockDim.x >> 6);
+    static_for<0, P>([&](auto kk) __attribute__((always_inline)) {
+        constexpr int k = decltype(kk)::value;
+        qms_pk_pair<C, EARLY, BETA>(wave + k * W, llr, B, iters, qmax, app_max, beta, qinv, flags, bits, soft, iters_used,
+                                    k * W);
+    });
+}
+
 template <class C>
 static int launch_qms_pk(const void* llr, int64_t B, const ldpc_params& p, uint8_t* bits, void* soft, int32_t* used,
                          hipStream_t st) {
     constexpr int CPW = (C::Z <= 32) ? 2 : 1;
-    const int64_t waves = (B + 2 * CPW - 1) / (2 * CPW);
-    const float qm = (float)p.qmax, am = (float)p.app_max, b = p.beta, qi = 1.0f / p.qstep;
     const bool es = (p.flags & LDPC_F_EARLY_STOP) != 0;
+    const int64_t waves = ((B + 2 * CPW - 1) / (2 * CPW) + (es ? QC_PK_PAIRS : 1) - 1) / (es ? QC_PK_PAIRS : 1);
+    const float qm = (float)p.qmax, am = (float)p.app_max, b = p.beta, qi = 1.0f / p.qstep;
     const int tpb = es ? pk_tpb<true>() : pk_tpb<false>();
     const unsigned blocks = (unsigned)((waves + tpb / 64 - 1) / (tpb / 64));
     const float* x = (const float*)llr;

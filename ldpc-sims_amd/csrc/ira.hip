@@ -46,8 +46,13 @@ struct IRASpec {
     int32_t *vn = nullptr, *vdeg = nullptr, *cn = nullptr, *cdeg = nullptr;  // device tables
 };
 
+// The tables are read-only for the whole decode: read through the constant address space so that every (uniform)
+// table read is a scalar load.  As plain global pointers the compiler could not rule out that the kernels' own stores
+// (app, states) alias them and read several rows with vector loads plus a wait and readfirstlane — one extra
+// dependent round trip per task (round 6).
+using cint32 = const __attribute__((address_space(4))) int32_t;
 struct IRADev {
-    const int32_t *vn, *vdeg, *cn, *cdeg;
+    cint32 *vn, *vdeg, *cn, *cdeg;
     int q, G, k, n, M;
 };
 
@@ -83,6 +88,12 @@ __device__ __forceinline__ bool ira_task(int T, int Bc, int& cw, int& task) {
 // per degree-8 task) instead of two masked passes (ira_vn_info)
 #ifndef IRA_VN_ROT
 #define IRA_VN_ROT 0
+#endif
+#ifndef IRA_VN_SCHED
+#define IRA_VN_SCHED 1
+#endif
+#ifndef IRA_CN_SCHED
+#define IRA_CN_SCHED 1
 #endif
 // c'[i] = c[(i + rho) mod D], rho < D, by log2(D) stages of selects (rotations compose additively mod D)
 template <int D>
@@ -148,31 +159,51 @@ struct IraEs {
 // summed as two masked passes (x + (-0) == x bit for bit, so a skipped entry changes nothing), 4 VALU per entry.
 // The state of check (ra, b) is addressed by a 32-bit byte offset from the codeword's first state (a scalar base).
 template <int D>
-__device__ __forceinline__ void ira_vn_info(const int32_t* __restrict__ row, int64_t vo, int64_t so, int pos,
+__device__ __forceinline__ void ira_vn_info(cint32* row, int64_t vo, int64_t so, int pos,
                                             const float* __restrict__ L, const IraState* __restrict__ S,
                                             float* __restrict__ app) {
     const int p = min(pos, kIZ - 1);
-    const float a = L[vo + p];
     const char* const Sb = reinterpret_cast<const char*>(S + so);
     float c[D];
     bool w[D];
     int wrapped = 0;
+#if IRA_DIAG_VN4
+    const float a = L[vo + p];
     static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
         constexpr int t = decltype(TT)::value;
-        const int e = row[t];  // wave-uniform: a scalar load
+        const int e = row[t];
         const int ra = e & 0xff, sh = (e >> 8) & 0x1ff, slot = e >> 17;
         int b = p + sh;
         w[t] = b >= kIZ;
         b -= w[t] ? kIZ : 0;
         wrapped += w[t];
-        const uint32_t off = (uint32_t)(ra * kIZ + b) * (uint32_t)sizeof(IraState);
-#if IRA_DIAG_VN4
         const float x = reinterpret_cast<const float*>(S)[so + (int64_t)ra * kIZ + b];
         c[t] = ira_c2v(IraState{x, x, (uint32_t)slot << 27}, slot);
-#else
-        c[t] = ira_c2v(ira_ld(reinterpret_cast<const IraState*>(Sb + off)), slot);
-#endif
     });
+#else
+    IraState st[D];
+    static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
+        constexpr int t = decltype(TT)::value;
+        const int e = row[t];  // wave-uniform: a scalar load
+        const int ra = e & 0xff, sh = (e >> 8) & 0x1ff;
+        int b = p + sh;
+        w[t] = b >= kIZ;
+        b -= w[t] ? kIZ : 0;
+        wrapped += w[t];
+        const uint32_t off = (uint32_t)(ra * kIZ + b) * (uint32_t)sizeof(IraState);
+        st[t] = ira_ld(reinterpret_cast<const IraState*>(Sb + off));
+    });
+    const float a = L[vo + p];
+    // IRA_VN_SCHED: every state load issued before the first is consumed (the scheduler had interleaved the first
+    // loads' decompression with the later loads' issue, behind a wait for the first ones: two round trips per task)
+#if IRA_VN_SCHED
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
+        constexpr int t = decltype(TT)::value;
+        c[t] = ira_c2v(st[t], row[t] >> 17);
+    });
+#endif
     float sum = a;
 #if IRA_VN_ROT
     const int rho = wrapped == 0 ? 0 : D - wrapped;
@@ -218,7 +249,7 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
         if (gi < t.G) {
             const int64_t vo = (int64_t)cw * t.n + (int64_t)gi * kIZ;
             const int d = t.vdeg[gi];
-            const int32_t* row = t.vn + gi * kIVS;
+            cint32* row = t.vn + gi * kIVS;
             static_for<1, MAXDV + 1>([&](auto DD) __attribute__((always_inline)) {
                 constexpr int D = decltype(DD)::value;
                 if (d == D) ira_vn_info<D>(row, vo, so, pos, L, S, app);
@@ -236,8 +267,12 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
             }
             const bool has1 = p1 < kIZ;  // j + 1 < M
             const int64_t i1 = so + (int64_t)r1 * kIZ + (has1 ? p1 : 0);
-            const float c0 = ira_c2v(ira_ld(S + i0), kIPS);
-            const float x1 = ira_c2v(ira_ld(S + i1), kIPS + 1);
+            const IraState s0 = ira_ld(S + i0), s1 = ira_ld(S + i1);
+#if IRA_VN_SCHED
+            __builtin_amdgcn_sched_barrier(0);  // both states and L in flight before the first use
+#endif
+            const float c0 = ira_c2v(s0, kIPS);
+            const float x1 = ira_c2v(s1, kIPS + 1);
             const float c1 = has1 ? x1 : -0.0f;  // x + (-0) == x bit for bit: the last parity has one check
             if (pos < kIZ) par.p[(int64_t)cw * par.stride + (int64_t)r * kIZ + pos] = (a + c0) + c1;
         }
@@ -266,7 +301,7 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
         const int64_t ao = (int64_t)cw * t.n;
         const int64_t si = (int64_t)cw * t.M + (int64_t)ra * kIZ + p;
         const int R = t.cdeg[ra];
-        const int32_t* row = t.cn + ra * kICS;
+        cint32* row = t.cn + ra * kICS;
         const IraState st = ira_ld(S + si);
         const float ap0 = prc[(int64_t)ra * kIZ + p];
         const int64_t pi = ra > 0 ? (int64_t)(ra - 1) * kIZ + p : (int64_t)(t.q - 1) * kIZ + (p > 0 ? p - 1 : 0);
@@ -280,7 +315,9 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
         float v[MAXR];
         static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
             constexpr int s = decltype(SS)::value;
-            if (s < R) {
+            // MAXR <= 8: every slot loads (a slot past R reads the zero-padded table entry: group 0 at this position,
+            // a cache hit, unused), so no load sits in a branch and all of them are in flight before the first wait
+            if (MAXR <= 8 || s < R) {
                 const int e = ent[s];
                 const int g = e & 0xff, sh = e >> 8;
                 int m = p - sh;
@@ -288,6 +325,9 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
                 v[s] = app[ao + (int64_t)g * kIZ + m];
             }
         });
+#if IRA_CN_SCHED
+        __builtin_amdgcn_sched_barrier(0);  // the state, both parity posteriors, L and every gather in flight first
+#endif
         if constexpr (ES) {  // the check on app_it: xor of its variables' decisions (z = app / 2)
             if (es.it >= 1) {
                 bool par = Num<float>::bit(0.5f * ap0);
@@ -570,7 +610,8 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
     const int64_t bc = ira_chunk(s, B, ns);
     const size_t set = ira_set_bytes(s, bc);
     auto a256 = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const IRADev t{s->vn, s->vdeg, s->cn, s->cdeg, s->q, s->G, s->k, s->n, s->M};
+    auto cst = [](const int32_t* x) { return (cint32*)x; };  // device tables, written once at graph creation
+    const IRADev t{cst(s->vn), cst(s->vdeg), cst(s->cn), cst(s->cdeg), s->q, s->G, s->k, s->n, s->M};
     const int soft_z = (p.flags & LDPC_F_SOFT_Z) ? 1 : 0;
     const unsigned tiles = (unsigned)((s->k + 1023) / 1024 + ((kIZ + 63) / 64) * ((s->q + 63) / 64));
     // tasks per workgroup: one task is a short wave (a few loads, one store); at one task per workgroup a launch is

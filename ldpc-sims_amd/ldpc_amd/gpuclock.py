@@ -13,6 +13,7 @@ import threading
 import time
 
 _NA = (None, "N/A")
+_INIT = []  # amdsmi initialised once per process (the library is process-global)
 
 
 def _num(x):
@@ -51,7 +52,9 @@ class ClockSampler:
         self._thr = None
         try:
             import amdsmi
-            amdsmi.amdsmi_init()
+            if not _INIT:
+                amdsmi.amdsmi_init()
+                _INIT.append(True)
             self._amdsmi = amdsmi
             self.h, self.bdf = _handle_for(device_index)
         except Exception as e:  # no amdsmi / no permission / no match: record why, measure nothing

@@ -1702,8 +1702,8 @@ namespace {
 // that decodes on different caller streams never share an auxiliary stream (no false dependence of one caller's join
 // on another's fork, and a graph capture open on stream A never absorbs a decode issued on stream B), and per host
 // thread so that no two threads interleave one set's fork / join.  At most kAuxSets sets per thread (the least
-// recently used is destroyed — hipStreamDestroy lets its pending work finish); a thread's sets are destroyed when
-// it exits.
+// recently used one outside any open graph capture is destroyed — hipStreamDestroy lets its pending work finish);
+// a thread's sets are destroyed when it exits.
 constexpr int kAux = 3;
 constexpr int kAuxSets = 16;
 struct Aux {
@@ -1750,18 +1750,31 @@ struct AuxPool {
             if (a.dev >= 0) a.release();
     }
 };
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+}
+bool any_capturing(const Aux& a) {
+    for (int i = 0; i < kAux; ++i)
+        if (a.s[i] && capturing(a.s[i])) return true;
+    return false;
+}
 Aux* aux_get(hipStream_t caller) {
     static thread_local AuxPool pool;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    Aux* lru = &pool.set[0];
+    Aux* lru = nullptr;
     for (Aux& a : pool.set) {
         if (a.dev == dev && a.caller == caller) {
             a.used = ++pool.clock;
             return &a;
         }
-        if (a.used < lru->used) lru = &a;
     }
+    // evict the least recently used set whose streams are not part of an open graph capture (destroying one
+    // would invalidate that capture); none free: the caller gets an error, not a broken graph
+    for (Aux& a : pool.set)
+        if ((!lru || a.used < lru->used) && (a.dev < 0 || !any_capturing(a))) lru = &a;
+    if (!lru) return nullptr;
     if (lru->dev >= 0) lru->release();
     if (!lru->create()) {
         lru->release();
@@ -1771,10 +1784,6 @@ Aux* aux_get(hipStream_t caller) {
     lru->caller = caller;
     lru->used = ++pool.clock;
     return lru;
-}
-bool capturing(hipStream_t s) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
 }
 }  // namespace
 

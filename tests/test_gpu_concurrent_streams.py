@@ -57,3 +57,33 @@ def test_interleaved_streams_equal_serial(monkeypatch):
             assert torch.equal(r["bits"], s["bits"]), (rnd, j)
             assert torch.equal(r["soft"].view(torch.int32), s["soft"].view(torch.int32)), (rnd, j)
             assert torch.equal(r["iters_used"], s["iters_used"]), (rnd, j)
+
+
+def test_more_caller_streams_than_auxiliary_sets(monkeypatch):
+    """The library keeps at most 16 auxiliary-stream sets per host thread, one per caller stream (csrc/qc.hip
+    aux_get); a 17th caller stream evicts the least recently used set while earlier decodes may still run on it.
+    Decodes forked from 20 caller streams, twice round, still equal the serial decodes."""
+    monkeypatch.setenv("LDPC_IRA_BUDGET_MB", "2")
+    jobs = []
+    for name, B in (("wifi648_12", 200), ("dvbs2_12", 5)):
+        H, _ = get_code(name)
+        enc = IRAEncoder(H) if name.startswith("dvbs2") else Encoder(H)
+        dec = ldpc_amd.get_decoder(H)
+        algo, kw = ("tanh", dict(clamp=10.0)) if name == "wifi648_12" else ("minsum", dict(clamp=20.0))
+        for rep in range(3):
+            jobs.append((dec, _llr(H, enc, B, 1.0 + rep, seed=100 + len(jobs), erase=0.02), algo, kw))
+    iters = 8
+    serial = []
+    for dec, x, algo, kw in jobs:
+        serial.append(dec.decode(x, iters, algo=algo, soft="z", **kw)["soft"].clone())
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(20)]
+    outs = []
+    for rnd in range(2):
+        for i, s in enumerate(streams):
+            j = (i + rnd) % len(jobs)
+            dec, x, algo, kw = jobs[j]
+            outs.append((j, dec.decode(x, iters, algo=algo, soft="z", stream=s, **kw)["soft"]))
+    torch.cuda.synchronize()
+    for k, (j, z) in enumerate(outs):
+        assert torch.equal(z.view(torch.int32), serial[j].view(torch.int32)), (k, j)

@@ -456,6 +456,8 @@ def roofline(n, E, B, launch_ms, args, kpath, m=None, iters=None):
         out.update(bound="memory-side (beyond L2, Infinity Cache included)", achieved=own, peak=IC_GATHER_GBPS,
                    unit="GB/s", frac=own / IC_GATHER_GBPS, hbm_frac=own / HBM_PEAK_GBPS, traffic=hbm_bytes,
                    traffic_note="2*FETCH_SIZE + WRITE_SIZE per launch: memory-side requests, Infinity-Cache hits included",
+                   bound_note="byte model as the yardstick; measured not byte-bound: 20 % fewer bytes per iteration "
+                              "ran at the same speed (DESIGN.md 3.8, profiles/r06/ab/ab_c4_ira_r6x.txt)",
                    bytes_per_codeword=ib, bytes_model="ira: iters*(12n + 36m) + 21n + 24m (csrc/ira.hip)")
         return out
     if kpath == "generic-csr" or "SQ_INSTS_VALU" not in c:

@@ -63,6 +63,19 @@ struct IraState {
 };
 static_assert(sizeof(IraState) == 12, "one dwordx3 per check state");
 
+#if IRA_DIAG_S8
+// the states as an array of 8-byte pairs indexed like the 12-byte array (the first two thirds of the buffer)
+__device__ __forceinline__ IraState ira_ld_i(const IraState* __restrict__ base, int64_t i) {
+    const float2 m = reinterpret_cast<const float2*>(base)[i];
+    return IraState{m.x, m.y, __float_as_uint(m.x) & 0x3ffu};
+}
+__device__ __forceinline__ void ira_st_i(IraState* __restrict__ base, int64_t i, const IraState& s) {
+    reinterpret_cast<float2*>(base)[i] = make_float2(s.m1, s.m2 + __uint_as_float(s.meta & 1u));
+}
+#else
+__device__ __forceinline__ IraState ira_ld_i(const IraState* __restrict__ base, int64_t i) { return base[i]; }
+__device__ __forceinline__ void ira_st_i(IraState* __restrict__ base, int64_t i, const IraState& s) { base[i] = s; }
+#endif
 __device__ __forceinline__ IraState ira_ld(const IraState* __restrict__ p) { return *p; }
 
 // c2v of slot `slot` from a check state: the argmin slot gets mag2, every other mag1; sign bit from meta
@@ -132,6 +145,20 @@ constexpr int kIraLanes = 384;
 #ifndef IRA_CNPAR
 #define IRA_CNPAR 1
 #endif
+#ifndef IRA_VN_PAIR
+#define IRA_VN_PAIR 0  // variable kernel: two information tasks of one degree with their loads in flight together (A/B knob)
+#endif
+#ifndef IRA_CN_EXACT
+// check kernel instances for at most 5 and 6 information slots: no gathers of padded slots (DVB-S2 1/2 has 5 per check;
+// the MAXR = 8 instance loads 8).  Config [4] 59.0 -> 60.3k cw/s (profiles/r06/ab/ab_c4_ira_r6x.txt)
+#define IRA_CN_EXACT 1
+#endif
+#ifndef IRA_CN_PF
+#define IRA_CN_PF 0  // check kernel: row ra + 1's loads issued before row ra's arithmetic (A/B knob)
+#endif
+#ifndef IRA_DIAG_S8
+#define IRA_DIAG_S8 0  // DIAGNOSTIC BUILD ONLY (wrong results): check states of 8 bytes (m1, m2; meta from m1's bits), to price 12 -> 8
+#endif
 
 // parity posteriors of codeword c, parity index j = r 360 + b: p[c stride + j]
 struct ParBuf {
@@ -159,15 +186,67 @@ struct IraEs {
 // summed as two masked passes (x + (-0) == x bit for bit, so a skipped entry changes nothing), 4 VALU per entry.
 // The state of check (ra, b) is addressed by a 32-bit byte offset from the codeword's first state (a scalar base).
 template <int D>
+struct VnIn {
+    IraState st[D];
+    bool w[D];
+    float a;
+};
+// the loads of one information task (its D check states and L), all issued before any use
+template <int D>
+__device__ __forceinline__ void ira_vn_load(cint32* row, int64_t vo, int64_t so, int pos, const float* __restrict__ L,
+                                            const IraState* __restrict__ S, VnIn<D>& in) {
+    const int p = min(pos, kIZ - 1);
+    const char* const Sb = reinterpret_cast<const char*>(S + so);
+    static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
+        constexpr int t = decltype(TT)::value;
+        const int e = row[t];  // wave-uniform: a scalar load
+        const int ra = e & 0xff, sh = (e >> 8) & 0x1ff;
+        int b = p + sh;
+        in.w[t] = b >= kIZ;
+        b -= in.w[t] ? kIZ : 0;
+#if IRA_DIAG_S8
+        (void)Sb;
+        in.st[t] = ira_ld_i(S, so + ra * kIZ + b);
+#else
+        const uint32_t off = (uint32_t)(ra * kIZ + b) * (uint32_t)sizeof(IraState);
+        in.st[t] = ira_ld(reinterpret_cast<const IraState*>(Sb + off));
+#endif
+    });
+    in.a = L[vo + p];
+}
+// app = L + the c2v in ascending check order, stored
+template <int D>
+__device__ __forceinline__ void ira_vn_sum(cint32* row, int64_t vo, int pos, float* __restrict__ app, const VnIn<D>& in) {
+    float c[D];
+    static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
+        constexpr int t = decltype(TT)::value;
+        c[t] = ira_c2v(in.st[t], row[t] >> 17);
+    });
+    float sum = in.a;
+#if IRA_VN_ROT
+    int wrapped = 0;
+#pragma unroll
+    for (int t = 0; t < D; ++t) wrapped += in.w[t];
+    const int rho = wrapped == 0 ? 0 : D - wrapped;
+    rotate_left<D>(c, rho);
+#pragma unroll
+    for (int t = 0; t < D; ++t) sum = sum + c[t];
+#else
+#pragma unroll
+    for (int t = 0; t < D; ++t) sum = sum + (in.w[t] ? c[t] : -0.0f);
+#pragma unroll
+    for (int t = 0; t < D; ++t) sum = sum + (in.w[t] ? -0.0f : c[t]);
+#endif
+    if (pos < kIZ) app[vo + pos] = sum;
+}
+template <int D>
 __device__ __forceinline__ void ira_vn_info(cint32* row, int64_t vo, int64_t so, int pos,
                                             const float* __restrict__ L, const IraState* __restrict__ S,
                                             float* __restrict__ app) {
+#if IRA_DIAG_VN4
     const int p = min(pos, kIZ - 1);
-    const char* const Sb = reinterpret_cast<const char*>(S + so);
     float c[D];
     bool w[D];
-    int wrapped = 0;
-#if IRA_DIAG_VN4
     const float a = L[vo + p];
     static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
         constexpr int t = decltype(TT)::value;
@@ -176,48 +255,25 @@ __device__ __forceinline__ void ira_vn_info(cint32* row, int64_t vo, int64_t so,
         int b = p + sh;
         w[t] = b >= kIZ;
         b -= w[t] ? kIZ : 0;
-        wrapped += w[t];
         const float x = reinterpret_cast<const float*>(S)[so + (int64_t)ra * kIZ + b];
         c[t] = ira_c2v(IraState{x, x, (uint32_t)slot << 27}, slot);
     });
+    float sum = a;
+#pragma unroll
+    for (int t = 0; t < D; ++t) sum = sum + (w[t] ? c[t] : -0.0f);
+#pragma unroll
+    for (int t = 0; t < D; ++t) sum = sum + (w[t] ? -0.0f : c[t]);
+    if (pos < kIZ) app[vo + pos] = sum;
 #else
-    IraState st[D];
-    static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
-        constexpr int t = decltype(TT)::value;
-        const int e = row[t];  // wave-uniform: a scalar load
-        const int ra = e & 0xff, sh = (e >> 8) & 0x1ff;
-        int b = p + sh;
-        w[t] = b >= kIZ;
-        b -= w[t] ? kIZ : 0;
-        wrapped += w[t];
-        const uint32_t off = (uint32_t)(ra * kIZ + b) * (uint32_t)sizeof(IraState);
-        st[t] = ira_ld(reinterpret_cast<const IraState*>(Sb + off));
-    });
-    const float a = L[vo + p];
+    VnIn<D> in;
+    ira_vn_load<D>(row, vo, so, pos, L, S, in);
     // IRA_VN_SCHED: every state load issued before the first is consumed (the scheduler had interleaved the first
     // loads' decompression with the later loads' issue, behind a wait for the first ones: two round trips per task)
 #if IRA_VN_SCHED
     __builtin_amdgcn_sched_barrier(0);
 #endif
-    static_for<0, D>([&](auto TT) __attribute__((always_inline)) {
-        constexpr int t = decltype(TT)::value;
-        c[t] = ira_c2v(st[t], row[t] >> 17);
-    });
+    ira_vn_sum<D>(row, vo, pos, app, in);
 #endif
-    float sum = a;
-#if IRA_VN_ROT
-    const int rho = wrapped == 0 ? 0 : D - wrapped;
-    rotate_left<D>(c, rho);
-#pragma unroll
-    for (int t = 0; t < D; ++t) sum = sum + c[t];
-#else
-    (void)wrapped;
-#pragma unroll
-    for (int t = 0; t < D; ++t) sum = sum + (w[t] ? c[t] : -0.0f);
-#pragma unroll
-    for (int t = 0; t < D; ++t) sum = sum + (w[t] ? -0.0f : c[t]);
-#endif
-    if (pos < kIZ) app[vo + pos] = sum;
 }
 
 // One task = one variable group (information group g < G, or parity row a = g - G) of one codeword; lanes =
@@ -244,16 +300,39 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
             }
         }
     }
-    for (int gi = tb * tpw; gi < T && gi < (tb + 1) * tpw; ++gi) {
+    const int gend = min(T, (tb + 1) * tpw);
+    for (int gi = tb * tpw; gi < gend; ++gi) {
         const int64_t so = (int64_t)cw * t.M;
         if (gi < t.G) {
             const int64_t vo = (int64_t)cw * t.n + (int64_t)gi * kIZ;
             const int d = t.vdeg[gi];
             cint32* row = t.vn + gi * kIVS;
+#if IRA_VN_PAIR
+            // two information tasks of one degree: both tasks' loads in flight together
+            const bool two = gi + 1 < gend && gi + 1 < t.G && t.vdeg[gi + 1] == d;
+#endif
             static_for<1, MAXDV + 1>([&](auto DD) __attribute__((always_inline)) {
                 constexpr int D = decltype(DD)::value;
-                if (d == D) ira_vn_info<D>(row, vo, so, pos, L, S, app);
+                if (d == D) {
+#if IRA_VN_PAIR
+                    if (two) {
+                        VnIn<D> i0, i1;
+                        ira_vn_load<D>(row, vo, so, pos, L, S, i0);
+                        ira_vn_load<D>(row + kIVS, vo + kIZ, so, pos, L, S, i1);
+                        __builtin_amdgcn_sched_barrier(0);
+                        ira_vn_sum<D>(row, vo, pos, app, i0);
+                        ira_vn_sum<D>(row + kIVS, vo + kIZ, pos, app, i1);
+                    } else {
+                        ira_vn_info<D>(row, vo, so, pos, L, S, app);
+                    }
+#else
+                    ira_vn_info<D>(row, vo, so, pos, L, S, app);
+#endif
+                }
             });
+#if IRA_VN_PAIR
+            gi += two ? 1 : 0;
+#endif
         } else if (!IRA_DIAG_NOPAR) {
             // parity p_j, j = r + q pos: checks j (its own (r, pos), slot kIPS) and j + 1 (slot kIPS + 1 there)
             const int r = pgrp > 0 ? min((gi - t.G + 1) * pgrp, t.q) - 1 : gi - t.G;
@@ -267,7 +346,7 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_vn(IRADev t, const float* __r
             }
             const bool has1 = p1 < kIZ;  // j + 1 < M
             const int64_t i1 = so + (int64_t)r1 * kIZ + (has1 ? p1 : 0);
-            const IraState s0 = ira_ld(S + i0), s1 = ira_ld(S + i1);
+            const IraState s0 = ira_ld_i(S, i0), s1 = ira_ld_i(S, i1);
 #if IRA_VN_SCHED
             __builtin_amdgcn_sched_barrier(0);  // both states and L in flight before the first use
 #endif
@@ -296,23 +375,29 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
     bool unsat = false;  // ES, it >= 1: some check of this lane's rows fails on app_it
     const int p = min(pos, kIZ - 1);
     const float* const prc = pr.p + (int64_t)cw * pr.stride;
+    const int64_t ao = (int64_t)cw * t.n;
+    const int r0 = tb * tpw, r1 = min(t.q, (tb + 1) * tpw);
     IraState prev = {0.0f, 0.0f, 0u};  // FUSE: the new state of the previous row at this position
-    for (int ra = tb * tpw; ra < t.q && ra < (tb + 1) * tpw; ++ra) {
-        const int64_t ao = (int64_t)cw * t.n;
+    struct In {
+        IraState st;
+        float ap0, ap1, lp;
+        float v[MAXR];
+    };
+    // every load of row ra: its state, both parity posteriors, L of parity (ra - 1, p) (FUSE) and the gathers
+    auto fetch = [&](int ra, In& in) __attribute__((always_inline)) {
         const int64_t si = (int64_t)cw * t.M + (int64_t)ra * kIZ + p;
         const int R = t.cdeg[ra];
         cint32* row = t.cn + ra * kICS;
-        const IraState st = ira_ld(S + si);
-        const float ap0 = prc[(int64_t)ra * kIZ + p];
+        in.st = ira_ld_i(S, si);
+        in.ap0 = prc[(int64_t)ra * kIZ + p];
         const int64_t pi = ra > 0 ? (int64_t)(ra - 1) * kIZ + p : (int64_t)(t.q - 1) * kIZ + (p > 0 ? p - 1 : 0);
-        const float ap1 = prc[pi];
-        const bool fuse = FUSE && ra > tb * tpw;  // parity (ra - 1, p): both its checks' new states are here
-        const float lp = fuse ? L[ao + t.k + (int64_t)(ra - 1) * kIZ + p] : 0.0f;
+        in.ap1 = prc[pi];
+        const bool fuse = FUSE && ra > r0;  // parity (ra - 1, p): both its checks' new states are here
+        in.lp = fuse ? L[ao + t.k + (int64_t)(ra - 1) * kIZ + p] : 0.0f;
         // the row's table entries as one scalar load before any use (inside the per-slot branches each entry was
         // its own load and wait, and each slot's posterior load waited on it)
         int ent[MAXR];
         static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) { ent[decltype(SS)::value] = row[decltype(SS)::value]; });
-        float v[MAXR];
         static_for<0, MAXR>([&](auto SS) __attribute__((always_inline)) {
             constexpr int s = decltype(SS)::value;
             // MAXR <= 8: every slot loads (a slot past R reads the zero-padded table entry: group 0 at this position,
@@ -322,12 +407,16 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
                 const int g = e & 0xff, sh = e >> 8;
                 int m = p - sh;
                 m += m < 0 ? kIZ : 0;
-                v[s] = app[ao + (int64_t)g * kIZ + m];
+                in.v[s] = app[ao + (int64_t)g * kIZ + m];
             }
         });
-#if IRA_CN_SCHED
-        __builtin_amdgcn_sched_barrier(0);  // the state, both parity posteriors, L and every gather in flight first
-#endif
+    };
+    auto update = [&](int ra, In& in) __attribute__((always_inline)) {
+        const int64_t si = (int64_t)cw * t.M + (int64_t)ra * kIZ + p;
+        const int R = t.cdeg[ra];
+        const IraState st = in.st;
+        const float ap0 = in.ap0, ap1 = in.ap1;
+        float* const v = in.v;
         if constexpr (ES) {  // the check on app_it: xor of its variables' decisions (z = app / 2)
             if (es.it >= 1) {
                 bool par = Num<float>::bit(0.5f * ap0);
@@ -375,14 +464,37 @@ __global__ __launch_bounds__(kIraLanes) void k_ira_cn(IRADev t, const float* __r
         meta |= ((sgn ^ f2u(vp0)) >> 31) << kIPS;
         if (has_prev) meta |= ((sgn ^ f2u(vp1)) >> 31) << (kIPS + 1);
         const IraState nst{mag1, mag2, meta};
-        if (pos < kIZ) S[si] = nst;
+        if (pos < kIZ) ira_st_i(S, si, nst);
         if constexpr (FUSE) {
-            if (fuse && pos < kIZ)
+            if (ra > r0 && pos < kIZ)
                 pw.p[(int64_t)cw * pw.stride + (int64_t)(ra - 1) * kIZ + pos] =
-                    (lp + ira_c2v(prev, kIPS)) + ira_c2v(nst, kIPS + 1);
+                    (in.lp + ira_c2v(prev, kIPS)) + ira_c2v(nst, kIPS + 1);
             prev = nst;
         }
+    };
+#if IRA_CN_PF
+    // software-pipelined: row ra + 1's loads are issued before row ra's arithmetic, so each wave keeps two rows of
+    // loads in flight (the kernel runs about one round of workgroups per launch: the loads in flight per wave, not
+    // the number of waves, set how much of the memory latency is hidden)
+    In cur;
+    fetch(r0, cur);
+    for (int ra = r0; ra < r1; ++ra) {
+        In nxt;
+        if (ra + 1 < r1) fetch(ra + 1, nxt);
+        __builtin_amdgcn_sched_barrier(0);
+        update(ra, cur);
+        cur = nxt;
     }
+#else
+    for (int ra = r0; ra < r1; ++ra) {
+        In in;
+        fetch(ra, in);
+#if IRA_CN_SCHED
+        __builtin_amdgcn_sched_barrier(0);  // the state, both parity posteriors, L and every gather in flight first
+#endif
+        update(ra, in);
+    }
+#endif
     if constexpr (ES) {  // this group's word (every thread of the workgroup gets here)
         const bool any = __syncthreads_or(unsat || es.it == 0);
         if (threadIdx.x == 0) es.flg[(int64_t)cw * es.ng + tb] = any ? 1 : 0;
@@ -673,7 +785,15 @@ int ira_decode(const IRASpec* s, const float* llr, int64_t B, const ldpc_params&
                 if (es_on) IRA_VN(16, true); else IRA_VN(16, false);
             }
             if (it == p.iters) break;  // the last VN pass is the final layer's posterior
+#if IRA_CN_EXACT
+            if (s->maxr <= 5) {
+                if (es_on) IRA_CN(5, true); else IRA_CN(5, false);
+            } else if (s->maxr <= 6) {
+                if (es_on) IRA_CN(6, true); else IRA_CN(6, false);
+            } else if (s->maxr <= 8) {
+#else
             if (s->maxr <= 8) {
+#endif
                 if (es_on) IRA_CN(8, true); else IRA_CN(8, false);
             } else {
                 if (es_on) IRA_CN(kICS, true); else IRA_CN(kICS, false);

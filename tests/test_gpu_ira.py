@@ -205,15 +205,21 @@ def _shaped_ira(q, G, degs, seed, Z=360):
     return _ira_code(groups, f"ira_q{q}_g{G}", n=k + m, k=k, q=q, Z=Z)
 
 
-@pytest.mark.parametrize("shape", ["r23_long", "short"])
+@pytest.mark.parametrize("shape", ["r23_long", "short", "six", "nine"])
 def test_other_ira_shapes_vs_oracle(shape):
     """Other IRA shapes through the same kernels: a rate-2/3-shaped normal frame (q = 60, 12 groups of degree 13 —
-    the 16-slot variable kernel — and 108 of degree 3) and a short one (q = 25, 20 groups): bits, z and iteration
-    counts bitwise against the oracle, fixed count and early stop."""
+    the 16-slot variable kernel — and 108 of degree 3; 8 information slots per check), a short one (q = 25, 20
+    groups; 4 slots: the 5-slot check kernel), one with 6 slots per check (the 6-slot check kernel) and one with 9
+    (the 24-slot check kernel, per-slot branches): bits, z and iteration counts bitwise against the oracle, fixed
+    count and early stop."""
     if shape == "r23_long":                                 # _llr's noise is set for rate 1/2: points shifted
         H, pts = _shaped_ira(60, 120, [13] * 12 + [3] * 108, seed=23), ((3.2, False), (4.0, True))
-    else:
+    elif shape == "short":
         H, pts = _shaped_ira(25, 20, [8] * 8 + [3] * 12, seed=7), ((1.0, False), (2.6, True))
+    elif shape == "six":
+        H, pts = _shaped_ira(20, 20, [8] * 10 + [4] * 10, seed=6), ((1.0, False), (2.6, True))
+    else:
+        H, pts = _shaped_ira(12, 18, [12] * 6 + [3] * 12, seed=9), ((1.5, False), (3.0, True))
     dec = ldpc_amd.get_decoder(H)
     assert dec.kernel_path(dec.params(20, "minsum", 20.0)) == "ira-z360"
     for ebn0, es in pts:

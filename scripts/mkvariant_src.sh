@@ -1,7 +1,8 @@
 #!/bin/bash
 # mkvariant_src.sh NAME FILE SRC "extra flags": abvar/NAME.so = the library with csrc/FILE replaced by SRC (another
 # revision of that file, e.g. `git show REV:ldpc-sims_amd/csrc/FILE > /tmp/x.hip`) built with the extra flags; the
-# other objects come from the in-tree build.  abvar/ is transient (git-ignored; delete it after the A/B).
+# other objects come from the in-tree build.  abvar/ is local only (git- and gpurun-ignored): for an A/B on the GPU
+# box build the variant there, `python ldpc-sims_amd/build.py --out build_variants/NAME.so -DKNOB=1`.
 set -e
 cd "$(dirname "$0")/.."
 name=$1; file=$2; src=$3; extra=$4

@@ -1816,6 +1816,7 @@ int aux_join(hipStream_t st, int n) {
 int qc_sp_fork(const float* llr, int64_t B, int n, int cpu, hipStream_t st, hipStream_t* s2) {
     uint32_t* zl = qc_sp_zlist();
     if (!zl) return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: no workspace");
+    if (cpu < 1 || cpu > 8) return set_error(LDPC_EHIP, "tanh-SP zero-LLR pass: %d codewords per unit (flag byte holds 8)", cpu);
     if (hipMemsetAsync(zl, 0, 4, st) != hipSuccess) return set_error(LDPC_EHIP, "zero-LLR list reset failed");
     const int64_t units = (B + cpu - 1) / cpu;
     k_sp_zero_scan<<<(unsigned)((units + 3) / 4), 256, 0, st>>>(llr, B, n, cpu, units, zl);

@@ -127,7 +127,7 @@ def main():
     total_cw = world * args.steps * B
     ranks = rank_evidence(world, rank, local, my_elapsed, wl.clock)
     value = total_cw / elapsed
-    roof = roofline(n, E, B, gpu_ms, args, wl.kpath, wl.m, wl.mean_iters)
+    roof = roofline(n, E, B, gpu_ms, args, wl.kpath, wl.m, wl.mean_iters, clock=wl.clock)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # CPU baseline at N=1 only
@@ -221,7 +221,7 @@ def run_leg(name, args, rank, local, world):
     rec = {"baseline_config": LEGS[name]["baseline"], "value": world * steps * wl.B / elapsed,
            "unit": "codewords/s", "n_gpus": world, "steps": steps, "warmup": 1,
            "ms_per_step": elapsed / steps * 1e3, "ms_per_launch": gpu_ms,
-           "config": wl.config_dict(world), "roofline": roofline(wl.n, wl.E, wl.B, gpu_ms, la, wl.kpath, wl.m, wl.mean_iters),
+           "config": wl.config_dict(world), "roofline": roofline(wl.n, wl.E, wl.B, gpu_ms, la, wl.kpath, wl.m, wl.mean_iters, clock=wl.clock),
            "mean_iters": wl.mean_iters, "clock": wl.clock, "ber": ber}
     if world > 1:
         rec["ranks"] = rank_evidence(world, rank, local, my_elapsed, wl.clock)
@@ -405,7 +405,7 @@ def ira_bytes_per_cw(n, m, iters):
     return iters * (12 * n + 36 * m) + 21 * n + 24 * m
 
 
-def roofline(n, E, B, launch_ms, args, kpath, m=None, iters=None):
+def roofline(n, E, B, launch_ms, args, kpath, m=None, iters=None, clock=None):
     """The decode launch against the resource that binds it.
 
     * Streaming (generic CSR) kernels move every message through HBM each iteration: bound "hbm",
@@ -474,6 +474,12 @@ def roofline(n, E, B, launch_ms, args, kpath, m=None, iters=None):
     b = "lds" if out["lds"]["frac"] > out["valu"]["frac"] else "valu"
     out.update(bound=b, achieved=out[b]["achieved"], peak=out[b]["peak"], unit=out[b]["unit"], frac=out[b]["frac"],
                traffic=hbm_bytes)
+    mhz = (clock or {}).get("clock_mhz")
+    if mhz:
+        # the on-chip peaks scale with the engine clock: the same fraction against the peak at the mean clock the
+        # timed loop ran at (a power-limited kernel runs below the 2.4 GHz the peak assumes)
+        out["frac_at_clock"] = out["frac"] * CLOCK_HZ / (mhz * 1e6)
+        out["clock_mhz"] = mhz
     return out
 
 

@@ -61,4 +61,10 @@ def test_bench_line_contract():
     assert "clock_mhz" in clk or "error" in clk, clk
     if "clock_mhz" in clk:
         assert 500 < clk["clock_mhz"] <= 2500 and clk["samples"] >= 1
+        # an on-chip bound (a counter record of this exact configuration: the full-size run) also carries its
+        # fraction at the clock the loop ran at (peaks scale with the clock)
+        r = d["roofline"]
+        if r["bound"] in ("lds", "valu"):
+            assert r["clock_mhz"] == clk["clock_mhz"]
+            assert abs(r["frac_at_clock"] - r["frac"] * 2400.0 / clk["clock_mhz"]) < 1e-9
     assert d["ranks"]["per_rank"][0]["clock"] == clk

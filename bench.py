@@ -60,8 +60,10 @@ def algorithmic_bytes_per_cw(n, E, iters, s_m=4, s_l=4):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=22)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 330 timed launches (30 passes over the 11 points, ~0.5 s): after the barrier / synchronize that open the
+    # timed loop the engine clock needs ~8 launches to recover, 4-5 % of a 22-launch loop
+    ap.add_argument("--steps", type=int, default=330)
+    ap.add_argument("--warmup", type=int, default=11)
     ap.add_argument("--code", default="wifi648_12")
     ap.add_argument("--algo", default="minsum")
     ap.add_argument("--iters", type=int, default=50)
@@ -169,7 +171,7 @@ def main():
             "data": f"synthetic: random info bits, systematic encoder, {args.mod} LLRs generated on device",
             "config": wl.config_dict(world),
             # engine clock / power over rank 0's timed loop (every rank's in ranks.per_rank[].clock): the
-            # headline kernel is power-limited, so throughput is quoted with the clock it ran at
+            # headline kernel runs below the other kernels' clock, so throughput is quoted with the clock it ran at
             "clock": wl.clock,
             "ranks": ranks,
             "roofline": roof,
@@ -178,6 +180,8 @@ def main():
             "side": side or None,
             "ber": ber,
         }
+        if getattr(wl, "step_trace_ms", None) is not None:
+            out["step_trace_ms"] = [round(x, 4) for x in wl.step_trace_ms]
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
@@ -186,12 +190,14 @@ def main():
 # BASELINE.json configs[2..4], each one short event-timed leg of this script (side.configs; never `value`)
 LEGS = {
     "config2": dict(code="wifi1944_56", algo="tanh", iters=50, batch=32768, mod="16qam-ofdm", ebn0="4:0.5:9",
-                    early_stop=False, baseline="configs[2]: tanh sum-product, (1944,5/6), 16-QAM OFDM front end"),
+                    early_stop=False, passes=4, warmup=11,
+                    baseline="configs[2]: tanh sum-product, (1944,5/6), 16-QAM OFDM front end"),
     "config3": dict(code="wifi1296_23", algo="qminsum", iters=20, batch=65536, mod="bpsk", ebn0="0:0.5:5",
-                    early_stop=True, qstep=1.0,
+                    early_stop=True, qstep=1.0, passes=30, warmup=11,
                     baseline="configs[3]: 5-bit LLR min-sum, (1296,2/3), 20 iters early termination"),
     "config4": dict(code="dvbs2_12", algo="minsum", iters=50, batch=4096, mod="bpsk", ebn0="0:0.5:2",
-                    early_stop=False, baseline="configs[4]: DVB-S2 64800 rate 1/2, 50 iters, batch sharded"),
+                    early_stop=False, passes=2, warmup=1,
+                    baseline="configs[4]: DVB-S2 64800 rate 1/2, 50 iters, batch sharded"),
 }
 
 
@@ -201,25 +207,27 @@ def leg_args(name, args):
     import argparse as _ap
     d = dict(vars(args))
     d.update(force_generic=False, alpha=1.0, qstep=1.0, clamp=20.0)
-    d.update({k: v for k, v in LEGS[name].items() if k != "baseline"})
+    d.update({k: v for k, v in LEGS[name].items() if k not in ("baseline", "passes", "warmup")})
     if args.leg_batch_scale != 1.0:  # tests only: a smaller batch (counter records then do not match)
         d["batch"] = max(64, int(d["batch"] * args.leg_batch_scale))
     return _ap.Namespace(**d)
 
 
 def run_leg(name, args, rank, local, world):
-    """One BASELINE config as a side leg: data resident in HBM, an untimed BER pass over its grid, one
-    warmup launch, then 2 launches per Eb/N0 point event-timed (so an early-stop leg's mean launch is the
-    sweep's mean), max over ranks; roofline from this leg's own counter record."""
+    """One BASELINE config as a side leg: data resident in HBM, an untimed BER pass over its grid, the leg's
+    warmup launches, then `passes` launches per Eb/N0 point event-timed (so an early-stop leg's mean launch is the
+    sweep's mean; passes sized for a timed loop of >= ~0.3 s, past the clock ramp after the pre-loop
+    synchronisation), max over ranks; roofline from this leg's own counter record."""
     import torch
     la = leg_args(name, args)
     wl = Workload(la, rank, local)
     ber = wl.ber()
     P = len(wl.ebn0)
-    steps = 2 * P
-    elapsed, my_elapsed, gpu_ms = wl.timed(steps, 1, world)
+    steps = LEGS[name]["passes"] * P
+    warm = LEGS[name]["warmup"]
+    elapsed, my_elapsed, gpu_ms = wl.timed(steps, warm, world)
     rec = {"baseline_config": LEGS[name]["baseline"], "value": world * steps * wl.B / elapsed,
-           "unit": "codewords/s", "n_gpus": world, "steps": steps, "warmup": 1,
+           "unit": "codewords/s", "n_gpus": world, "steps": steps, "warmup": warm,
            "ms_per_step": elapsed / steps * 1e3, "ms_per_launch": gpu_ms,
            "config": wl.config_dict(world), "roofline": roofline(wl.n, wl.E, wl.B, gpu_ms, la, wl.kpath, wl.m, wl.mean_iters, clock=wl.clock),
            "mean_iters": wl.mean_iters, "clock": wl.clock, "ber": ber}
@@ -320,21 +328,28 @@ class Workload:
         import torch
         import torch.distributed as dist
         from ldpc_amd.dist import max_over_ranks
+        from ldpc_amd.gpuclock import ClockSampler
         P = len(self.ebn0)
+        # engine clock / power while the loop runs; built before the warmup so that amdsmi's start-up is not an
+        # idle gap between the warmup and the timed loop (after an idle gap the engine clock ramps up again over
+        # the first ~8 launches: DESIGN §5)
+        sampler = ClockSampler(torch.cuda.current_device())
         for w in range(warmup):
             self.step(self.llrs[w % P])
         torch.cuda.synchronize()
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
-        from ldpc_amd.gpuclock import ClockSampler
-        sampler = ClockSampler(torch.cuda.current_device())   # engine clock / power while the loop runs
         if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
         with sampler:
             t0 = time.perf_counter()
             ev0.record(self.stream)
+            trace = [] if os.environ.get("LDPC_BENCH_STEP_TRACE") else None   # diagnostic: one event per step
             for s in range(steps):
+                if trace is not None:
+                    trace.append(torch.cuda.Event(enable_timing=True))
+                    trace[-1].record(self.stream)
                 self.step(self.llrs[s % P])
             ev1.record(self.stream)
             torch.cuda.synchronize()
@@ -343,6 +358,9 @@ class Workload:
             dist.barrier()
         mine = time.perf_counter() - t0
         gpu_ms = ev0.elapsed_time(ev1) / max(steps, 1)
+        if trace is not None:
+            ends = trace[1:] + [ev1]
+            self.step_trace_ms = [a.elapsed_time(b) for a, b in zip(trace, ends)]
         self.clock = sampler.summary()
         self.clock["window_s"] = t1 - t0
         return max_over_ranks(mine, device="cuda"), mine, gpu_ms
@@ -477,7 +495,7 @@ def roofline(n, E, B, launch_ms, args, kpath, m=None, iters=None, clock=None):
     mhz = (clock or {}).get("clock_mhz")
     if mhz:
         # the on-chip peaks scale with the engine clock: the same fraction against the peak at the mean clock the
-        # timed loop ran at (a power-limited kernel runs below the 2.4 GHz the peak assumes)
+        # timed loop ran at (a loaded chip runs below the 2.4 GHz the peak assumes)
         out["frac_at_clock"] = out["frac"] * CLOCK_HZ / (mhz * 1e6)
         out["clock_mhz"] = mhz
     return out
@@ -525,7 +543,7 @@ def side_measurements(H, dec, llrs, B, args, kpath):
     for w in range(3):
         run(llrs[w % len(llrs)])
     torch.cuda.synchronize()
-    steps = 2 * len(llrs)
+    steps = 6 * len(llrs)   # ~0.25 s: past the clock ramp after the synchronize above
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for s in range(steps):

@@ -48,7 +48,8 @@ def test_bench_line_contract():
         assert (c["code"], c["algo"], c["iters"], c["mod"], c["early_stop"], c["batch_per_gpu"]) == \
             (code, algo, iters, mod, es, b), name
         P = len(lg["ber"]["ebn0_db"])
-        assert lg["steps"] == 2 * P and lg["value"] > 0 and lg["ms_per_launch"] > 0
+        passes = {"config2": 4, "config3": 30, "config4": 2}[name]   # bench.LEGS: timed loops of >= ~0.3 s
+        assert lg["steps"] == passes * P and lg["value"] > 0 and lg["ms_per_launch"] > 0
         assert abs(lg["value"] - b / (lg["ms_per_step"] / 1e3)) <= 1e-6 * lg["value"]
         for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_ms"):
             assert k in lg["roofline"], (name, k)

@@ -15,7 +15,7 @@ data-path exchange, so scaling is weak).
 line and exits with the worst rank's code; under a launcher, WORLD_SIZE must equal N.
 
 The other BASELINE.json configs run as short legs of the same script after the headline, reported under
-``side.configs`` (never ``value``), each event-timed over two launches per Eb/N0 point with its own
+``side.configs`` (never ``value``), each event-timed over LEGS[...]['passes'] launches per Eb/N0 point with its own
 roofline from profiles/counters.json: configs[2] (1944,5/6) tanh-SP 50 it on 16-QAM OFDM LLRs, B=32,768;
 configs[3] (1296,2/3) 5-bit min-sum <=20 it early stop, B=65,536; configs[4] DVB-S2 64800 rate 1/2 min-sum
 50 it, B=4,096 per GPU.  Under torchrun (N>1) the config [4] leg runs on every rank — the BASELINE

@@ -67,8 +67,11 @@ class ClockSampler:
             clks = [m["current_gfxclk"]]
         return m, clks
 
+    # the firmware's throttle residency counters: per accumulation tick, whether the package sat at that limit
+    LIMITS = ("ppt", "socket_thm", "vr_thm", "hbm_thm", "prochot")
+
     def _acc(self, m):
-        return (_num(m.get("accumulation_counter")), _num(m.get("ppt_residency_acc")))
+        return (_num(m.get("accumulation_counter")),) + tuple(_num(m.get(f"{k}_residency_acc")) for k in self.LIMITS)
 
     def _run(self):
         while not self._stop.is_set():
@@ -108,7 +111,7 @@ class ClockSampler:
             return {"error": self.err, "source": "amdsmi gpu_metrics"}
         s = self.samples
         out = {"source": "amdsmi gpu_metrics: current_gfxclks (mean over XCDs), current_socket_power, "
-                         "ppt_residency_acc; polled every %.0f ms over the timed loop" % (self.period * 1e3),
+                         "throttle residency accumulators; polled every %.0f ms over the timed loop" % (self.period * 1e3),
                "pci": self.bdf, "samples": len(s)}
         if s:
             mean = [x[1] for x in s]
@@ -118,9 +121,16 @@ class ClockSampler:
             if pw:
                 out["socket_power_w"] = sum(pw) / len(pw)
         a0, a1 = self._acc0, self._acc1
-        if a0 and a1 and None not in a0 + a1 and a1[0] > a0[0]:
-            # the firmware counts, per accumulation tick, whether the package sat at its power limit (PPT)
-            out["ppt_limited_frac"] = (a1[1] - a0[1]) / (a1[0] - a0[0])
+        if a0 and a1 and None not in (a0[0], a1[0]) and a1[0] > a0[0]:
+            ticks = a1[0] - a0[0]
+            lim = {k: (a1[i + 1] - a0[i + 1]) / ticks for i, k in enumerate(self.LIMITS)
+                   if a0[i + 1] is not None and a1[i + 1] is not None}
+            if "ppt" in lim:
+                out["ppt_limited_frac"] = lim["ppt"]   # the package at its power limit
+            if lim:
+                out["limit_residency"] = lim           # every throttle limit's share of the loop
+            # amdsmi's averaged power reading lags the load: over windows of tens of ms it under-reads
+            out["note"] = "power and residency are firmware averages; meaningful over windows of >= ~0.3 s"
         if self.err is not None:
             out["error"] = self.err
         return out

@@ -106,10 +106,11 @@ class ClockSampler:
                 pass
         return False
 
-    def summary(self) -> dict:
+    def summary(self, since=None) -> dict:
+        """`since`: a time.perf_counter() value; samples taken before it (a warmup's tail) are left out."""
         if self.err is not None and not self.samples:
             return {"error": self.err, "source": "amdsmi gpu_metrics"}
-        s = self.samples
+        s = self.samples if since is None else [x for x in self.samples if x[0] >= since]
         out = {"source": "amdsmi gpu_metrics: current_gfxclks (mean over XCDs), current_socket_power, "
                          "throttle residency accumulators; polled every %.0f ms over the timed loop" % (self.period * 1e3),
                "pci": self.bdf, "samples": len(s)}

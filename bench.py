@@ -369,9 +369,11 @@ class Workload:
             ev1.record(self.stream)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-        if dist.is_initialized():
-            dist.barrier()
-        mine = time.perf_counter() - t0
+            if dist.is_initialized():
+                dist.barrier()
+            # the closing synchronize and barrier are inside the bracket; the sampler's stop (a thread join of up to
+            # one poll period and a last amdsmi read) is not: it had added ~0.7 ms to a 20-launch loop
+            mine = time.perf_counter() - t0
         gpu_ms = ev0.elapsed_time(ev1) / max(steps, 1)
         if trace is not None:
             ends = trace[1:] + [ev1]
